@@ -1,0 +1,28 @@
+/* ORACLE -- TEST INFRASTRUCTURE ONLY (see fet_oracle.c / css_oracle.c headers). */
+#ifndef GD_ORACLE_H
+#define GD_ORACLE_H
+#include <stdint.h>
+
+#define ORC_NSAMPLES 100 /* bootstrap replicates, cFisher.c:62 / threadfisher.c:171 */
+#define ORC_ERR_BOUNDS (-5)
+
+int orc_population_size(const int *pos, int len);
+int orc_threaded_window_end(int regend, int wsize, int wstep);
+int orc_serial_window_end(int regend, int wsize, int wstep);
+uint64_t orc_window_state(uint64_t seed, uint64_t stream, long w);
+void orc_state_words(uint64_t x, unsigned short st[3]);
+
+unsigned long orc_binomial(unsigned long n, unsigned long k);
+double orc_fet_p(int a, int b, int c, int d);
+double orc_fet(int a, int b, int c, int d);
+double orc_fet_score(int a, int b, int c, int d);
+void orc_fet_counts(const double *av, const double *bv, int i, int asize, int bsize, int *f);
+double orc_percentile(double *s, int n, double perc);
+void orc_fet_window(const double *av, const double *bv, int asize, int bsize, int npos, double perc,
+                    unsigned short st[3], double *fetscores, double *samples, double *out2);
+int orc_fet_scan(const double *avals, const double *bvals, const int *apos, const int *bpos, int regend,
+                 int wsize, int wstep, int alen, int blen, double perc, uint64_t seed, int serial,
+                 double *scores, double *stddev);
+void orc_nrand48_stream(uint64_t x0, int n, long *out);
+
+#endif
