@@ -1,0 +1,537 @@
+/*
+ * gd_api.hip -- C ABI glue: device contexts, workspaces, the device-resident
+ * batched scans and the reference-signature host entry points (include/gdscan.h).
+ *
+ * The host entry points mirror the reference drivers' contracts:
+ *   threadcompute() threadfisher.c:47-100 / threadcss.c:52-109   (window set: GD_WINDOWS_THREADED)
+ *   compute()       cFisher.c:38-115     / css.c:49-156          (window set: GD_WINDOWS_SERIAL)
+ * input arrays are read-only, outputs are written only at computed windows, and
+ * the caller owns every buffer.  Unlike the reference they return a status, do
+ * not print, and are reentrant.
+ */
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/gdscan.h"
+#include "gd_common.h"
+#include "gd_internal.h"
+
+/* kernels (gd_fet_kernels.hip, gd_css_kernels.hip, gd_synth.hip) */
+__global__ void k_binom_table(uint64_t *tab);
+__global__ void k_popsize(gd_chrom_dev *ch, const int32_t *apos, const int32_t *bpos, unsigned *flags);
+__global__ void k_bounds(const gd_chrom_dev *ch, const int32_t *apos, const int32_t *bpos, int wsize, int wstep,
+                         int32_t *lo_a, int32_t *hi_a, int32_t *lo_b, unsigned *flags);
+__global__ void k_snp_fet(const gd_chrom_dev *ch, const double *avals, const double *bvals, const uint64_t *binom,
+                          double *snp_score);
+template <int BLOCK, bool GLOBAL_SCRATCH>
+__global__ void k_fet_window_general(const gd_chrom_dev *ch, int nchrom, const int32_t *wlist,
+                                     const unsigned *wlist_count, int64_t wtotal, const int32_t *lo_a,
+                                     const int32_t *hi_a, const int32_t *lo_b, const double *avals,
+                                     const double *bvals, const double *snp_score, const uint64_t *binom,
+                                     double perc, double *scores, double *stddev, unsigned *flags,
+                                     int32_t *huge_list, unsigned *huge_count, double *gscratch,
+                                     int64_t gscratch_n);
+int gd_fet_window_fast_launch(const gd_chrom_dev *ch, int nchrom, int64_t wtotal, const int32_t *lo_a,
+                              const int32_t *hi_a, const int32_t *lo_b, const double *snp_score, double perc,
+                              double *scores, double *stddev, unsigned *flags, int32_t *slow_list,
+                              unsigned *slow_count, hipStream_t s);
+int gd_css_pipeline(struct gd_ctx *ctx, const gd_chrom_dev *d_ch, const std::vector<gd_chrom_dev> &h_ch,
+                    int64_t wtotal, const double *avals, const double *bvals, int wsize, int wstep, int treshold,
+                    int runs, double *scores, double *p, hipStream_t s);
+int gd_synth_launch(int chrom, int nsnp, int asize, int bsize, uint64_t seed, const double *freq_table,
+                    double *avals, double *bvals, int32_t *apos, int32_t *bpos, hipStream_t s);
+
+/* ------------------------------------------------------------------ errors */
+static thread_local std::string g_err;
+static std::atomic<uint64_t> g_seed{GD_DEFAULT_SEED};
+static thread_local float g_stage_ms[GD_NSTAGES];
+
+static int fail(int code, const std::string &msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                     \
+  do {                                                                                    \
+    hipError_t e_ = (expr);                                                               \
+    if (e_ != hipSuccess) return fail(GD_ERR_HIP, std::string(#expr ": ") + hipGetErrorString(e_)); \
+  } while (0)
+
+/* ----------------------------------------------------------------- context */
+struct gd_ctx {
+  int device = 0;
+  std::mutex mu;
+  hipStream_t stream = nullptr; /* used by the host entry points */
+  char *ws = nullptr;
+  size_t ws_cap = 0;
+  double *gscratch = nullptr;
+  size_t gscratch_cap = 0; /* doubles */
+  uint64_t *binom = nullptr;
+  /* host-API staging buffers (device) */
+  char *io = nullptr;
+  size_t io_cap = 0;
+  hipEvent_t ev[GD_NSTAGES + 1] = {};
+  unsigned *h_flags = nullptr; /* pinned */
+};
+
+static int ctx_init(gd_ctx *c, int device) {
+  c->device = device;
+  HIP_TRY(hipSetDevice(device));
+  HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+  HIP_TRY(hipMalloc(&c->binom, sizeof(uint64_t) * GD_BINOM_ENTRIES));
+  hipLaunchKernelGGL(k_binom_table, dim3((GD_BINOM_ENTRIES + 255) / 256), dim3(256), 0, c->stream, c->binom);
+  HIP_TRY(hipGetLastError());
+  for (auto &e : c->ev) HIP_TRY(hipEventCreate(&e));
+  HIP_TRY(hipHostMalloc(&c->h_flags, 64));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return GD_OK;
+}
+
+extern "C" gd_ctx *gd_ctx_create(int device) {
+  gd_ctx *c = new gd_ctx();
+  if (ctx_init(c, device) != GD_OK) {
+    gd_ctx_destroy(c);
+    return nullptr;
+  }
+  return c;
+}
+
+extern "C" void gd_ctx_destroy(gd_ctx *c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  (void)hipFree(c->ws);
+  (void)hipFree(c->gscratch);
+  (void)hipFree(c->binom);
+  (void)hipFree(c->io);
+  for (auto &e : c->ev)
+    if (e) (void)hipEventDestroy(e);
+  if (c->h_flags) (void)hipHostFree(c->h_flags);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+static gd_ctx *default_ctx(int *status) {
+  static std::mutex m;
+  static std::vector<gd_ctx *> ctxs;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+  std::lock_guard<std::mutex> g(m);
+  if ((int)ctxs.size() <= dev) ctxs.resize(dev + 1, nullptr);
+  if (!ctxs[dev]) {
+    ctxs[dev] = gd_ctx_create(dev);
+    if (!ctxs[dev]) {
+      *status = GD_ERR_HIP;
+      return nullptr;
+    }
+  }
+  *status = GD_OK;
+  return ctxs[dev];
+}
+
+static int grow(char **buf, size_t *cap, size_t need) {
+  if (need <= *cap) return GD_OK;
+  if (*buf) HIP_TRY(hipFree(*buf));
+  *buf = nullptr;
+  *cap = 0;
+  size_t n = std::max(need, (size_t)1 << 20);
+  n += n / 4;
+  HIP_TRY(hipMalloc(buf, n));
+  *cap = n;
+  return GD_OK;
+}
+
+/* -------------------------------------------------------------- windows */
+extern "C" int gd_window_count(int regend, int wsize, int wstep, int window_set) {
+  if (wsize <= 0 || wstep <= 0 || regend <= 0) return 0;
+  int64_t end = 0;
+  if (window_set == GD_WINDOWS_SERIAL) {
+    /* while (start + wsize <= regend + wstep)  (cFisher.c:81, css.c:117) */
+    const int64_t lim = (int64_t)regend + wstep - wsize;
+    end = lim >= 0 ? lim / wstep + 1 : 0;
+  } else {
+    /* threadfisher.c:55-58,191-239 / threadcss.c:60-63,226-276 */
+    const int num_windows = regend / wstep - 3;
+    const int num_tasks = num_windows / 100;
+    if (num_tasks <= 0) return 0;
+    for (int64_t t = 0; t <= num_tasks; ++t) {
+      int64_t stop = (t + 1) * 100 * (int64_t)wstep + (wsize - wstep);
+      if (stop >= regend) stop = (int64_t)regend + wstep;
+      const int64_t first = t * 100 * (int64_t)wstep;
+      if (first + wsize > stop) continue;
+      const int64_t last = (stop - wsize) / wstep; /* largest w with w*wstep + wsize <= stop */
+      end = std::max(end, last + 1);
+    }
+  }
+  return (int)std::min<int64_t>(end, regend / wstep);
+}
+
+/* -------------------------------------------------------- workspace carve */
+struct Carve {
+  char *base;
+  size_t off = 0;
+  template <class T>
+  T *take(size_t n) {
+    off = (off + 255) & ~(size_t)255;
+    T *p = (T *)(base ? base + off : nullptr);
+    off += n * sizeof(T);
+    return p;
+  }
+};
+
+struct ScanPlan {
+  std::vector<gd_chrom_dev> h;
+  int64_t wtotal = 0;
+  int64_t elems_a = 0, elems_b = 0;
+  int32_t max_alen = 0, max_blen = 0;
+};
+
+static int make_plan(const gd_chrom *chroms, int nchrom, int wsize, int wstep, int window_set, ScanPlan *pl) {
+  if (nchrom < 0 || (nchrom > 0 && !chroms)) return fail(GD_ERR_ARG, "bad chromosome list");
+  if (wsize <= 0 || wstep <= 0) return fail(GD_ERR_ARG, "wsize and wstep must be positive");
+  if (window_set != GD_WINDOWS_THREADED && window_set != GD_WINDOWS_SERIAL)
+    return fail(GD_ERR_ARG, "unknown window set");
+  pl->h.resize(nchrom);
+  int64_t wb = 0;
+  for (int c = 0; c < nchrom; ++c) {
+    const gd_chrom &s = chroms[c];
+    if (s.alen < 0 || s.blen < 0 || s.a_off < 0 || s.b_off < 0) return fail(GD_ERR_ARG, "negative extent");
+    gd_chrom_dev &d = pl->h[c];
+    std::memset(&d, 0, sizeof d);
+    d.a_off = s.a_off;
+    d.b_off = s.b_off;
+    d.alen = s.alen;
+    d.blen = s.blen;
+    d.regend = s.regend;
+    d.w_out = s.w_out;
+    d.seed = s.seed;
+    d.wend = (s.alen > 0 && s.blen > 0) ? gd_window_count(s.regend, wsize, wstep, window_set) : 0;
+    d.w_base = wb;
+    wb += d.wend;
+    pl->elems_a = std::max<int64_t>(pl->elems_a, s.a_off + s.alen);
+    pl->elems_b = std::max<int64_t>(pl->elems_b, s.b_off + s.blen);
+    pl->max_alen = std::max(pl->max_alen, s.alen);
+    pl->max_blen = std::max(pl->max_blen, s.blen);
+  }
+  if (wb > INT32_MAX) return fail(GD_ERR_ARG, "too many windows in one batch");
+  pl->wtotal = wb;
+  return GD_OK;
+}
+
+static int flags_to_status(unsigned f) {
+  if (f & (GD_FLAG_UNSORTED_A | GD_FLAG_UNSORTED_B)) return fail(GD_ERR_UNSORTED, "positions are not sorted");
+  if (f & GD_FLAG_B_BOUNDS) return fail(GD_ERR_BOUNDS, "a window's B slice runs past blen");
+  if (f & GD_FLAG_BAD_SIZE) return fail(GD_ERR_SIZE, "empty population or unsupported window size");
+  return GD_OK;
+}
+
+/* --------------------------------------------------------------- FET scan */
+static int fet_scan_locked(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, const double *avals,
+                           const double *bvals, const int32_t *apos, const int32_t *bpos, int wsize, int wstep,
+                           double perc, int window_set, double *scores, double *stddev, hipStream_t s) {
+  if (!(perc >= 0.0 && perc <= 1.0)) return fail(GD_ERR_ARG, "percentile must lie in [0, 1]");
+  ScanPlan pl;
+  int st = make_plan(chroms, nchrom, wsize, wstep, window_set, &pl);
+  if (st) return st;
+  for (float &m : g_stage_ms) m = 0.f;
+  if (pl.wtotal == 0) return GD_OK;
+  HIP_TRY(hipSetDevice(ctx->device));
+
+  Carve cv{nullptr};
+  auto layout = [&](Carve &k, gd_chrom_dev **d_ch, unsigned **flags, int32_t **lo_a, int32_t **hi_a,
+                    int32_t **lo_b, double **snp, int32_t **list, int32_t **huge) {
+    *d_ch = k.take<gd_chrom_dev>(nchrom);
+    *flags = k.take<unsigned>(16);
+    *lo_a = k.take<int32_t>(pl.wtotal);
+    *hi_a = k.take<int32_t>(pl.wtotal);
+    *lo_b = k.take<int32_t>(pl.wtotal);
+    *snp = k.take<double>(pl.elems_a);
+    *list = k.take<int32_t>(pl.wtotal);
+    *huge = k.take<int32_t>(pl.wtotal);
+  };
+  gd_chrom_dev *d_ch;
+  unsigned *flags;
+  int32_t *lo_a, *hi_a, *lo_b, *list, *huge;
+  double *snp;
+  layout(cv, &d_ch, &flags, &lo_a, &hi_a, &lo_b, &snp, &list, &huge);
+  if ((st = grow(&ctx->ws, &ctx->ws_cap, cv.off))) return st;
+  Carve real{ctx->ws};
+  layout(real, &d_ch, &flags, &lo_a, &hi_a, &lo_b, &snp, &list, &huge);
+  unsigned *list_count = flags + 4, *huge_count = flags + 8;
+
+  HIP_TRY(hipMemcpyAsync(d_ch, pl.h.data(), sizeof(gd_chrom_dev) * nchrom, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemsetAsync(flags, 0, 16 * sizeof(unsigned), s));
+  HIP_TRY(hipEventRecord(ctx->ev[0], s));
+  hipLaunchKernelGGL(k_popsize, dim3(nchrom), dim3(64), 0, s, d_ch, apos, bpos, flags);
+  {
+    const int64_t mx = std::max(pl.max_alen, pl.max_blen) + 1;
+    const unsigned gx = (unsigned)std::min<int64_t>((mx + 255) / 256, 2048);
+    hipLaunchKernelGGL(k_bounds, dim3(gx, nchrom, 2), dim3(256), 0, s, d_ch, apos, bpos, wsize, wstep, lo_a,
+                       hi_a, lo_b, flags);
+  }
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipEventRecord(ctx->ev[1], s));
+  {
+    const unsigned gx = (unsigned)std::min<int64_t>((pl.max_alen + 255) / 256, 4096);
+    hipLaunchKernelGGL(k_snp_fet, dim3(std::max(gx, 1u), nchrom), dim3(256), 0, s, d_ch, avals, bvals,
+                       ctx->binom, snp);
+  }
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipEventRecord(ctx->ev[2], s));
+  st = gd_fet_window_fast_launch(d_ch, nchrom, pl.wtotal, lo_a, hi_a, lo_b, snp, perc, scores, stddev, flags,
+                                 list, list_count, s);
+  if (st) return st;
+  HIP_TRY(hipEventRecord(ctx->ev[3], s));
+  {
+    /* windows the fast path declined: literal one-workgroup-per-window path */
+    const unsigned gx = (unsigned)std::min<int64_t>(pl.wtotal, 4096);
+    hipLaunchKernelGGL((k_fet_window_general<64, false>), dim3(gx), dim3(64), 0, s, d_ch, nchrom, list,
+                       list_count, pl.wtotal, lo_a, hi_a, lo_b, avals, bvals, snp, ctx->binom, perc, scores,
+                       stddev, flags, huge, huge_count, (double *)nullptr, (int64_t)0);
+  }
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipEventRecord(ctx->ev[4], s));
+  HIP_TRY(hipMemcpyAsync(ctx->h_flags, flags, 16 * sizeof(unsigned), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  const unsigned nhuge = ctx->h_flags[8];
+  if (nhuge > 0 && !(ctx->h_flags[0] & ~GD_FLAG_B_BOUNDS)) {
+    /* windows too dense for LDS: one 256-thread workgroup each, scratch in HBM */
+    const int64_t nmax = std::max<int64_t>(pl.max_alen, 1);
+    int64_t np2 = 1;
+    while (np2 < nmax) np2 <<= 1;
+    const int64_t per = np2 + 2 * nmax + (nmax + 1) / 2 + 2;
+    const int slots = 4;
+    if ((size_t)(per * slots) > ctx->gscratch_cap) {
+      (void)hipFree(ctx->gscratch);
+      ctx->gscratch = nullptr;
+      ctx->gscratch_cap = 0;
+      HIP_TRY(hipMalloc(&ctx->gscratch, sizeof(double) * per * slots));
+      ctx->gscratch_cap = per * slots;
+    }
+    hipLaunchKernelGGL((k_fet_window_general<256, true>), dim3(slots), dim3(256), 0, s, d_ch, nchrom, huge,
+                       huge_count, (int64_t)0, lo_a, hi_a, lo_b, avals, bvals, snp, ctx->binom, perc, scores,
+                       stddev, flags, (int32_t *)nullptr, (unsigned *)nullptr, ctx->gscratch, per);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(ctx->h_flags, flags, 16 * sizeof(unsigned), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+  }
+  float ms;
+  for (int i = 0; i < GD_NSTAGES; ++i)
+    if (hipEventElapsedTime(&ms, ctx->ev[i], ctx->ev[i + 1]) == hipSuccess) g_stage_ms[i] = ms;
+  return flags_to_status(ctx->h_flags[0]);
+}
+
+extern "C" int gd_fet_scan_device(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, const double *avals,
+                                  const double *bvals, const int32_t *apos, const int32_t *bpos, int wsize,
+                                  int wstep, double perc, int window_set, double *scores, double *stddev,
+                                  void *hip_stream) {
+  if (!ctx) return fail(GD_ERR_ARG, "null context");
+  std::lock_guard<std::mutex> g(ctx->mu);
+  return fet_scan_locked(ctx, chroms, nchrom, avals, bvals, apos, bpos, wsize, wstep, perc, window_set, scores,
+                         stddev, (hipStream_t)hip_stream);
+}
+
+/* one chromosome from host memory: H2D, device scan, D2H of the outputs */
+template <class Run>
+static int host_scan(const double *avals, const double *bvals, const int *apos, const int *bpos, int regend,
+                     int wsize, int wstep, int alen, int blen, double *out0, double *out1, Run run) {
+  if (wsize <= 0 || wstep <= 0) return fail(GD_ERR_ARG, "wsize and wstep must be positive");
+  if (alen < 0 || blen < 0) return fail(GD_ERR_ARG, "negative array length");
+  if (alen == 0 || blen == 0 || regend <= 0) return GD_OK;
+  if (!avals || !bvals || !apos || !bpos || !out0 || !out1) return fail(GD_ERR_ARG, "null buffer");
+  int st;
+  gd_ctx *ctx = default_ctx(&st);
+  if (!ctx) return fail(GD_ERR_HIP, "no HIP device available");
+  std::lock_guard<std::mutex> g(ctx->mu);
+  HIP_TRY(hipSetDevice(ctx->device));
+  const int64_t nwin = regend / wstep;
+  Carve cv{nullptr};
+  auto lay = [&](Carve &k, double **av, double **bv, int32_t **ap, int32_t **bp, double **o0, double **o1) {
+    *av = k.take<double>(alen);
+    *bv = k.take<double>(blen);
+    *ap = k.take<int32_t>(alen);
+    *bp = k.take<int32_t>(blen);
+    *o0 = k.take<double>(std::max<int64_t>(nwin, 1));
+    *o1 = k.take<double>(std::max<int64_t>(nwin, 1));
+  };
+  double *av, *bv, *o0, *o1;
+  int32_t *ap, *bp;
+  lay(cv, &av, &bv, &ap, &bp, &o0, &o1);
+  if ((st = grow(&ctx->io, &ctx->io_cap, cv.off))) return st;
+  Carve real{ctx->io};
+  lay(real, &av, &bv, &ap, &bp, &o0, &o1);
+  hipStream_t s = ctx->stream;
+  HIP_TRY(hipMemcpyAsync(av, avals, sizeof(double) * alen, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(bv, bvals, sizeof(double) * blen, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(ap, apos, sizeof(int32_t) * alen, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(bp, bpos, sizeof(int32_t) * blen, hipMemcpyHostToDevice, s));
+  if (nwin > 0) {
+    HIP_TRY(hipMemcpyAsync(o0, out0, sizeof(double) * nwin, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(o1, out1, sizeof(double) * nwin, hipMemcpyHostToDevice, s));
+  }
+  gd_chrom ch;
+  std::memset(&ch, 0, sizeof ch);
+  ch.alen = alen;
+  ch.blen = blen;
+  ch.regend = regend;
+  ch.seed = g_seed.load();
+  st = run(ctx, &ch, av, bv, ap, bp, o0, o1, s);
+  if (st) return st;
+  if (nwin > 0) {
+    HIP_TRY(hipMemcpyAsync(out0, o0, sizeof(double) * nwin, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(out1, o1, sizeof(double) * nwin, hipMemcpyDeviceToHost, s));
+  }
+  HIP_TRY(hipStreamSynchronize(s));
+  return GD_OK;
+}
+
+extern "C" int gd_fet_scan_host(const double *avals, const double *bvals, const int *apos, const int *bpos,
+                                int regend, int wsize, int wstep, int alen, int blen, double perc, uint64_t seed,
+                                int window_set, double *scores, double *stddev) {
+  return host_scan(avals, bvals, apos, bpos, regend, wsize, wstep, alen, blen, scores, stddev,
+                   [&](gd_ctx *ctx, gd_chrom *ch, double *av, double *bv, int32_t *ap, int32_t *bp, double *o0,
+                       double *o1, hipStream_t s) {
+                     ch->seed = seed;
+                     return fet_scan_locked(ctx, ch, 1, av, bv, ap, bp, wsize, wstep, perc, window_set, o0,
+                                            o1, s);
+                   });
+}
+
+extern "C" int gd_fet_threadcompute(const double *avals, const double *bvals, const int *apos, const int *bpos,
+                                    int regstart, int regend, int wsize, int wstep, int alen, int blen,
+                                    double perc, double *scores, double *stddev) {
+  (void)regstart; /* ignored by the reference too (threadfisher.c:110) */
+  return gd_fet_scan_host(avals, bvals, apos, bpos, regend, wsize, wstep, alen, blen, perc, g_seed.load(),
+                          GD_WINDOWS_THREADED, scores, stddev);
+}
+
+extern "C" int gd_fet_compute(const double *avals, const double *bvals, const int *apos, const int *bpos,
+                              int regstart, int regend, int wsize, int wstep, int alen, int blen, double perc,
+                              double *scores, double *stddev) {
+  (void)regstart; /* ignored by the reference too (cFisher.c:60) */
+  return gd_fet_scan_host(avals, bvals, apos, bpos, regend, wsize, wstep, alen, blen, perc, g_seed.load(),
+                          GD_WINDOWS_SERIAL, scores, stddev);
+}
+
+/* --------------------------------------------------------------- CSS scan */
+static int css_scan_locked(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, const double *avals,
+                           const double *bvals, const int32_t *apos, const int32_t *bpos, int wsize, int wstep,
+                           int treshold, int runs, int window_set, double *scores, double *p, hipStream_t s) {
+  ScanPlan pl;
+  int st = make_plan(chroms, nchrom, wsize, wstep, window_set, &pl);
+  if (st) return st;
+  for (float &m : g_stage_ms) m = 0.f;
+  if (pl.wtotal == 0) return GD_OK;
+  HIP_TRY(hipSetDevice(ctx->device));
+  Carve cv{nullptr};
+  auto layout = [&](Carve &k, gd_chrom_dev **d_ch, unsigned **flags, int32_t **lo_a, int32_t **hi_a,
+                    int32_t **lo_b) {
+    *d_ch = k.take<gd_chrom_dev>(nchrom);
+    *flags = k.take<unsigned>(16);
+    *lo_a = k.take<int32_t>(pl.wtotal);
+    *hi_a = k.take<int32_t>(pl.wtotal);
+    *lo_b = k.take<int32_t>(pl.wtotal);
+  };
+  gd_chrom_dev *d_ch;
+  unsigned *flags;
+  int32_t *lo_a, *hi_a, *lo_b;
+  layout(cv, &d_ch, &flags, &lo_a, &hi_a, &lo_b);
+  const size_t fixed = cv.off;
+  if ((st = grow(&ctx->ws, &ctx->ws_cap, fixed))) return st;
+  Carve real{ctx->ws};
+  layout(real, &d_ch, &flags, &lo_a, &hi_a, &lo_b);
+  HIP_TRY(hipMemcpyAsync(d_ch, pl.h.data(), sizeof(gd_chrom_dev) * nchrom, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemsetAsync(flags, 0, 16 * sizeof(unsigned), s));
+  HIP_TRY(hipEventRecord(ctx->ev[0], s));
+  hipLaunchKernelGGL(k_popsize, dim3(nchrom), dim3(64), 0, s, d_ch, apos, bpos, flags);
+  {
+    const int64_t mx = std::max(pl.max_alen, pl.max_blen) + 1;
+    const unsigned gx = (unsigned)std::min<int64_t>((mx + 255) / 256, 2048);
+    hipLaunchKernelGGL(k_bounds, dim3(gx, nchrom, 2), dim3(256), 0, s, d_ch, apos, bpos, wsize, wstep, lo_a,
+                       hi_a, lo_b, flags);
+  }
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipEventRecord(ctx->ev[1], s));
+  /* pull the population sizes back: the CSS kernels are specialised on m */
+  HIP_TRY(hipMemcpyAsync(pl.h.data(), d_ch, sizeof(gd_chrom_dev) * nchrom, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(ctx->h_flags, flags, 16 * sizeof(unsigned), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  if ((st = flags_to_status(ctx->h_flags[0]))) return st;
+  st = gd_css_pipeline(ctx, d_ch, pl.h, pl.wtotal, avals, bvals, wsize, wstep, treshold, runs, scores, p, s);
+  if (st) return st;
+  HIP_TRY(hipMemcpyAsync(ctx->h_flags, flags, 16 * sizeof(unsigned), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  return flags_to_status(ctx->h_flags[0]);
+}
+
+/* CSS needs the window bounds and sizes laid out by css_scan_locked; the
+ * pipeline reads them back from the context's workspace */
+extern "C" int gd_css_scan_device(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, const double *avals,
+                                  const double *bvals, const int32_t *apos, const int32_t *bpos, int wsize,
+                                  int wstep, int treshold, int runs, int window_set, double *scores, double *p,
+                                  void *hip_stream) {
+  if (!ctx) return fail(GD_ERR_ARG, "null context");
+  std::lock_guard<std::mutex> g(ctx->mu);
+  return css_scan_locked(ctx, chroms, nchrom, avals, bvals, apos, bpos, wsize, wstep, treshold, runs, window_set,
+                         scores, p, (hipStream_t)hip_stream);
+}
+
+extern "C" int gd_css_scan_host(const double *avals, const double *bvals, const int *apos, const int *bpos,
+                                int regend, int wsize, int wstep, int alen, int blen, int treshold, int runs,
+                                uint64_t seed, int window_set, double *scores, double *p) {
+  return host_scan(avals, bvals, apos, bpos, regend, wsize, wstep, alen, blen, scores, p,
+                   [&](gd_ctx *ctx, gd_chrom *ch, double *av, double *bv, int32_t *ap, int32_t *bp, double *o0,
+                       double *o1, hipStream_t s) {
+                     ch->seed = seed;
+                     return css_scan_locked(ctx, ch, 1, av, bv, ap, bp, wsize, wstep, treshold, runs, window_set,
+                                            o0, o1, s);
+                   });
+}
+
+extern "C" int gd_css_threadcompute(const double *avals, const double *bvals, const int *apos, const int *bpos,
+                                    int regstart, int regend, int wsize, int wstep, int alen, int blen,
+                                    int treshold, int runs, int drosophila, int mds, double *scores, double *p) {
+  (void)regstart;
+  if (drosophila != 0 || mds != 0)
+    return fail(GD_ERR_ARG, "only the count metric (drosophila=0) with classical MDS (mds=0) is implemented");
+  return gd_css_scan_host(avals, bvals, apos, bpos, regend, wsize, wstep, alen, blen, treshold, runs,
+                          g_seed.load(), GD_WINDOWS_THREADED, scores, p);
+}
+
+extern "C" int gd_css_compute(const double *avals, const double *bvals, const int *apos, const int *bpos,
+                              int regstart, int regend, int wsize, int wstep, int alen, int blen, int treshold,
+                              int runs, int drosophila, int mds, double *scores, double *p) {
+  (void)regstart;
+  if (drosophila != 0 || mds != 0)
+    return fail(GD_ERR_ARG, "only the count metric (drosophila=0) with classical MDS (mds=0) is implemented");
+  return gd_css_scan_host(avals, bvals, apos, bpos, regend, wsize, wstep, alen, blen, treshold, runs,
+                          g_seed.load(), GD_WINDOWS_SERIAL, scores, p);
+}
+
+/* ------------------------------------------------------------- utilities */
+extern "C" void gd_set_seed(uint64_t seed) { g_seed.store(seed); }
+extern "C" uint64_t gd_get_seed(void) { return g_seed.load(); }
+extern "C" const char *gd_last_error(void) { return g_err.c_str(); }
+extern "C" int gd_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+extern "C" int gd_last_stage_ms(float *ms, int n) {
+  for (int i = 0; i < n && i < GD_NSTAGES; ++i) ms[i] = g_stage_ms[i];
+  return GD_NSTAGES;
+}
+
+extern "C" int gd_synth_device(int chrom, int nsnp, int asize, int bsize, uint64_t seed, const double *freq_table,
+                               double *avals, double *bvals, int32_t *apos, int32_t *bpos, void *hip_stream) {
+  if (nsnp <= 0 || asize <= 0 || bsize <= 0) return fail(GD_ERR_ARG, "bad synthetic sizes");
+  return gd_synth_launch(chrom, nsnp, asize, bsize, seed, freq_table, avals, bvals, apos, bpos,
+                         (hipStream_t)hip_stream);
+}

@@ -1,0 +1,466 @@
+/*
+ * gd_fet_kernels.hip -- HIP/CDNA4 kernels of the Fisher-exact-test window scan.
+ *
+ * Pipeline (one stream, no host round trip):
+ *   k_popsize        get_population_size() per chromosome      comparative.c:25-34
+ *   k_bounds         slide_right() for every window at once:    comparative.c:49-71
+ *                    one coalesced pass over the positions; element i owns the
+ *                    windows whose start (or inclusive stop) falls between
+ *                    pos[i-1] and pos[i]
+ *   k_snp_fet        fetcount() + fet() + -log10 once per SNP    cFisher.c:180-184
+ *                    (the reference recomputes each SNP in every one of the
+ *                    ~wsize/wstep windows covering it; the value depends only on
+ *                    the SNP's four counts, so computing it once is exact)
+ *   k_fet_window_*   percentile + 100-replicate bootstrap std   cFisher.c:136-144, 547-597
+ * All FP arithmetic is compiled with -ffp-contract=off (the reference build has no FMA).
+ */
+#include "gd_common.h"
+#include "gd_internal.h"
+
+namespace {
+
+__device__ __forceinline__ int64_t fdiv(int64_t a, int64_t b) { return a >= 0 ? a / b : -((-a + b - 1) / b); }
+__device__ __forceinline__ int64_t cdiv(int64_t a, int64_t b) { return -fdiv(-a, b); }
+
+__device__ __forceinline__ uint64_t binom_at(const uint64_t *tab, int n, int k) {
+  if (n >= 0 && k >= 0 && k <= n && n <= GD_BINOM_NMAX) return tab[gd_binom_index(n, k)];
+  return gd_binomial_ref((uint64_t)(int64_t)n, (uint64_t)(int64_t)k);
+}
+
+/* binomial lookups go through a kernel-local table pointer */
+struct BinomTab {
+  const uint64_t *t;
+  __device__ __forceinline__ uint64_t operator()(int n, int k) const { return binom_at(t, n, k); }
+};
+
+__device__ double fet_p_two_tailed(int a, int b, int c, int d, const uint64_t *tab) {
+  BinomTab B{tab};
+  const int tie = (a + b == c + d) || (a + c == b + d);
+  int f[4] = {a, b, c, d};
+  gd_table_min_to_a(f);
+  const double p0 = GD_FET_TABLE_P(B, f[0], f[1], f[2], f[3]);
+  double tot = p0, step = p0;
+  while (f[0] > 0) {
+    f[1]++;
+    f[2]++;
+    step = (1.0 * f[0] * f[3]) / (double)(f[1] * f[2]) * step;
+    tot += step;
+    f[0]--;
+    f[3]--;
+  }
+  if (tie) {
+    tot = 2 * tot;
+  } else {
+    gd_table_opposite_extreme(f);
+    gd_table_min_to_a(f);
+    double far = GD_FET_TABLE_P(B, f[0], f[1], f[2], f[3]);
+    while (far < p0) {
+      tot += far;
+      if (f[1] == 0 || f[2] == 0) break;
+      f[0]++;
+      f[3]++;
+      far = (1.0 * f[1] * f[2]) / (double)(f[0] * f[3]) * far;
+      f[1]--;
+      f[2]--;
+    }
+  }
+  if (tot > 1) tot = 1;
+  return tot;
+}
+
+/* fetcount(): exact double compares against 3 and -3 (cFisher.c:208-238) */
+__device__ __forceinline__ double snp_score_raw(const double *a, int asize, const double *b, int bsize,
+                                                const uint64_t *tab) {
+  int f0 = 0, f1 = 0, f2 = 0, f3 = 0;
+  for (int k = 0; k < asize; ++k) {
+    const double v = a[k];
+    f0 += (v == 3.0);
+    f1 += (v == -3.0);
+  }
+  for (int k = 0; k < bsize; ++k) {
+    const double v = b[k];
+    f2 += (v == 3.0);
+    f3 += (v == -3.0);
+  }
+  return gd_fet_score_from_p(fet_p_two_tailed(f0, f1, f2, f3, tab));
+}
+
+__device__ __forceinline__ int chrom_of(const gd_chrom_dev *ch, int nchrom, int64_t g) {
+  int lo = 0, hi = nchrom - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (ch[mid].w_base <= g)
+      lo = mid;
+    else
+      hi = mid - 1;
+  }
+  return lo;
+}
+
+}  // namespace
+
+/* ------------------------------------------------------------------------ */
+__global__ void k_binom_table(uint64_t *tab) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= GD_BINOM_ENTRIES) return;
+  int n = 0;
+  while ((n + 1) * (n + 2) / 2 <= e) ++n;
+  const int k = e - n * (n + 1) / 2;
+  tab[e] = gd_binomial_ref((uint64_t)n, (uint64_t)k);
+}
+
+/* get_population_size(): leading run of pos[0], bounded by the array length */
+__global__ void __launch_bounds__(64) k_popsize(gd_chrom_dev *ch, const int32_t *apos, const int32_t *bpos,
+                                                unsigned *flags) {
+  gd_chrom_dev &d = ch[blockIdx.x];
+  const int lane = threadIdx.x;
+  int sizes[2];
+  for (int pop = 0; pop < 2; ++pop) {
+    const int32_t *p = pop ? bpos + d.b_off : apos + d.a_off;
+    const int len = pop ? d.blen : d.alen;
+    int size = len;
+    if (len > 0) {
+      const int32_t p0 = p[0];
+      for (int base = 0; base < len; base += 64) {
+        const int i = base + lane;
+        const unsigned long long m = __ballot(i < len && p[i] != p0);
+        if (m) {
+          size = base + __ffsll((long long)m) - 1;
+          break;
+        }
+      }
+    }
+    sizes[pop] = size;
+  }
+  if (lane == 0) {
+    d.asize = sizes[0];
+    d.bsize = sizes[1];
+    d.nrows = 0;
+    if (d.wend > 0 && (sizes[0] <= 0 || sizes[1] <= 0)) atomicOr(flags, GD_FLAG_BAD_SIZE);
+    if (sizes[0] > 0 && sizes[1] > 0) {
+      const int ra = d.alen / sizes[0], rb = d.blen / sizes[1];
+      d.nrows = ra < rb ? ra : rb;
+    }
+  }
+}
+
+/* slide_right() for all windows: lo = first idx with pos >= start,
+ * hi = first idx with pos > start + wsize (inclusive end).  Grid (x, chrom, pop). */
+__global__ void __launch_bounds__(256) k_bounds(const gd_chrom_dev *ch, const int32_t *apos, const int32_t *bpos,
+                                                int wsize, int wstep, int32_t *lo_a, int32_t *hi_a,
+                                                int32_t *lo_b, unsigned *flags) {
+  const gd_chrom_dev &d = ch[blockIdx.y];
+  const int pop = blockIdx.z;
+  const int64_t wend = d.wend;
+  if (wend <= 0) return;
+  const int64_t len = pop ? d.blen : d.alen;
+  const int32_t *pos = pop ? bpos + d.b_off : apos + d.a_off;
+  int32_t *lo = (pop ? lo_b : lo_a) + d.w_base;
+  int32_t *hi = hi_a + d.w_base;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= len; i += stride) {
+    const int64_t p = (i < len) ? pos[i] : 0;
+    const int64_t pp = (i > 0) ? pos[i - 1] : 0;
+    if (i > 0 && i < len && p < pp) atomicOr(flags, pop ? GD_FLAG_UNSORTED_B : GD_FLAG_UNSORTED_A);
+    int64_t f = (i == 0) ? 0 : fdiv(pp, wstep) + 1;
+    int64_t l = (i == len) ? wend - 1 : fdiv(p, wstep);
+    if (f < 0) f = 0;
+    if (l > wend - 1) l = wend - 1;
+    for (int64_t w = f; w <= l; ++w) lo[w] = (int32_t)i;
+    if (pop == 0) {
+      f = (i == 0) ? 0 : cdiv(pp - wsize, wstep);
+      l = (i == len) ? wend - 1 : cdiv(p - wsize, wstep) - 1;
+      if (f < 0) f = 0;
+      if (l > wend - 1) l = wend - 1;
+      for (int64_t w = f; w <= l; ++w) hi[w] = (int32_t)i;
+    }
+  }
+}
+
+/* one thread per SNP row: counts -> Zar two-tailed p -> -log10 */
+__global__ void __launch_bounds__(256) k_snp_fet(const gd_chrom_dev *ch, const double *avals, const double *bvals,
+                                                 const uint64_t *binom, double *snp_score) {
+  const gd_chrom_dev &d = ch[blockIdx.y];
+  const int nrows = d.nrows, asize = d.asize, bsize = d.bsize;
+  if (d.wend <= 0) return;
+  const double *a = avals + d.a_off;
+  const double *b = bvals + d.b_off;
+  double *out = snp_score + d.a_off;
+  for (int s = blockIdx.x * blockDim.x + threadIdx.x; s < nrows; s += gridDim.x * blockDim.x)
+    out[s] = snp_score_raw(a + (int64_t)s * asize, asize, b + (int64_t)s * bsize, bsize, binom);
+}
+
+/* ------------------------------------------------------------------------ */
+/* General window path: one workgroup per window, literal semantics.         */
+/*   - scores gathered from snp_score when the window's A and B slices start  */
+/*     on the same SNP row, else recomputed from the raw slices              */
+/*   - ascending sort: bitonic (no NaN) or glibc-2.35 msort order (NaN)      */
+/*   - bootstrap: the nrand48 stream is consumed in order, BLOCK positions   */
+/*     per step, rejections compacted with a block scan                      */
+/* ------------------------------------------------------------------------ */
+namespace {
+
+template <int BLOCK>
+__device__ int block_incl_scan(int v, int *sh, int *total) {
+  const int t = threadIdx.x;
+  sh[t] = v;
+  __syncthreads();
+  for (int off = 1; off < BLOCK; off <<= 1) {
+    const int add = (t >= off) ? sh[t - off] : 0;
+    __syncthreads();
+    sh[t] += add;
+    __syncthreads();
+  }
+  const int r = sh[t];
+  *total = sh[BLOCK - 1];
+  __syncthreads();
+  return r;
+}
+
+/* glibc 2.35 qsort == top-down merge sort, left run wins ties (cmp <= 0) */
+__device__ void msort_glibc(double *a, double *tmp, int n) {
+  struct Frame {
+    int off, n, stage;
+  };
+  Frame st[64];
+  int sp = 0;
+  st[sp++] = {0, n, 0};
+  while (sp) {
+    Frame &fr = st[sp - 1];
+    if (fr.n <= 1) {
+      --sp;
+      continue;
+    }
+    const int n1 = fr.n / 2;
+    if (fr.stage == 0) {
+      fr.stage = 1;
+      st[sp++] = {fr.off, n1, 0};
+    } else if (fr.stage == 1) {
+      fr.stage = 2;
+      st[sp++] = {fr.off + n1, fr.n - n1, 0};
+    } else {
+      double *b1 = a + fr.off, *b2 = a + fr.off + n1;
+      int c1 = n1, c2 = fr.n - n1, o = 0;
+      while (c1 > 0 && c2 > 0) {
+        const double x = *b1, y = *b2;
+        const int cmp = (x > y) - (x < y);
+        if (cmp <= 0) {
+          tmp[o++] = x;
+          ++b1;
+          --c1;
+        } else {
+          tmp[o++] = y;
+          ++b2;
+          --c2;
+        }
+      }
+      while (c1 > 0) {
+        tmp[o++] = *b1++;
+        --c1;
+      }
+      for (int i = 0; i < o; ++i) a[fr.off + i] = tmp[i];
+      --sp;
+    }
+  }
+}
+
+template <int BLOCK>
+__device__ void bitonic_sort_pad(double *s, int n, int np2) {
+  for (int i = n + threadIdx.x; i < np2; i += BLOCK) s[i] = __builtin_inf();
+  __syncthreads();
+  for (int k = 2; k <= np2; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = threadIdx.x; i < np2; i += BLOCK) {
+        const int ixj = i ^ j;
+        if (ixj > i) {
+          const double x = s[i], y = s[ixj];
+          const bool up = (i & k) == 0;
+          if (up ? (x > y) : (x < y)) {
+            s[i] = y;
+            s[ixj] = x;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+}  // namespace
+
+template <int BLOCK, bool GLOBAL_SCRATCH>
+__global__ void __launch_bounds__(BLOCK)
+    k_fet_window_general(const gd_chrom_dev *ch, int nchrom, const int32_t *wlist, const unsigned *wlist_count,
+                         int64_t wtotal, const int32_t *lo_a, const int32_t *hi_a, const int32_t *lo_b,
+                         const double *avals, const double *bvals, const double *snp_score,
+                         const uint64_t *binom, double perc, double *scores, double *stddev, unsigned *flags,
+                         int32_t *huge_list, unsigned *huge_count, double *gscratch, int64_t gscratch_n) {
+  __shared__ double sh_rep[GD_NREP];
+  __shared__ int sh_scan[BLOCK];
+  __shared__ uint64_t sh_x;
+  __shared__ int sh_pick[2];
+  __shared__ int sh_nan;
+  constexpr int LDS_N = GLOBAL_SCRATCH ? 1 : GD_GEN_LDS_N;
+  __shared__ double sh_s[LDS_N], sh_smp[LDS_N], sh_tmp[LDS_N];
+  __shared__ uint32_t sh_hist[LDS_N];
+
+  if (*flags & (GD_FLAG_UNSORTED_A | GD_FLAG_UNSORTED_B | GD_FLAG_BAD_SIZE)) return;
+  const int tid = threadIdx.x;
+  const int64_t count = wlist ? (int64_t)*wlist_count : wtotal;
+  /* per-thread jump map: position P -> P + tid + 1 */
+  const gd_affine jmp = gd_lcg_jump((uint64_t)tid + 1);
+
+  for (int64_t it = blockIdx.x; it < count; it += gridDim.x) {
+    const int64_t g = wlist ? (int64_t)wlist[it] : it;
+    const int c = chrom_of(ch, nchrom, g);
+    const gd_chrom_dev &d = ch[c];
+    const int64_t w = g - d.w_base;
+    const int asize = d.asize, bsize = d.bsize;
+    const int lo = lo_a[g], hi = hi_a[g], lb = lo_b[g];
+    const int n = (hi - lo) / asize;
+    if (n <= 0) continue;
+    if ((int64_t)lb + (int64_t)n * bsize > d.blen) {
+      if (tid == 0) atomicOr(flags, GD_FLAG_B_BOUNDS);
+      continue;
+    }
+    int np2 = 1;
+    while (np2 < n) np2 <<= 1;
+    double *S, *smp, *tmp;
+    uint32_t *hist;
+    if (GLOBAL_SCRATCH) {
+      if ((int64_t)np2 + 2 * (int64_t)n + (n + 1) / 2 + 1 > gscratch_n) {
+        if (tid == 0) atomicOr(flags, GD_FLAG_BAD_SIZE);
+        continue;
+      }
+      double *base = gscratch + (int64_t)blockIdx.x * gscratch_n;
+      S = base;
+      smp = base + np2;
+      tmp = smp + n;
+      hist = (uint32_t *)(tmp + n);
+    } else {
+      if (np2 > LDS_N) {
+        if (tid == 0) huge_list[atomicAdd(huge_count, 1u)] = (int32_t)g;
+        continue;
+      }
+      S = sh_s;
+      smp = sh_smp;
+      tmp = sh_tmp;
+      hist = sh_hist;
+    }
+
+    /* 1. per-SNP scores of the window, in window order */
+    const bool aligned = (lo % asize == 0) && (lb % bsize == 0) && (lo / asize == lb / bsize) &&
+                         (lo / asize + n <= d.nrows);
+    if (tid == 0) sh_nan = 0;
+    __syncthreads();
+    int has_nan = 0;
+    for (int i = tid; i < n; i += BLOCK) {
+      double v;
+      if (aligned)
+        v = snp_score[d.a_off + lo / asize + i];
+      else
+        v = snp_score_raw(avals + d.a_off + lo + (int64_t)i * asize, asize,
+                          bvals + d.b_off + lb + (int64_t)i * bsize, bsize, binom);
+      S[i] = v;
+      has_nan |= (v != v);
+    }
+    if (has_nan) sh_nan = 1;
+    __syncthreads();
+    const bool nan_mode = sh_nan != 0;
+
+    /* 2. ascending sort (qsort in percentile(), cFisher.c:140) */
+    if (nan_mode) {
+      if (tid == 0) msort_glibc(S, tmp, n);
+      __syncthreads();
+    } else {
+      bitonic_sort_pad<BLOCK>(S, n, np2);
+    }
+
+    const int idx = gd_perc_index(n, perc);
+    const double delta = gd_perc_delta(n, perc, idx);
+    const int idx1 = (idx + 1 < n) ? idx + 1 : idx;
+    const double wscore = gd_perc_mix(delta, S[idx], S[idx1]);
+
+    /* 3. bootstrap: 100 replicates of n draws from the sorted scores */
+    const gd_randint rd = gd_randint_make((uint32_t)n);
+    uint64_t xP = gd_window_state(d.seed, GD_STREAM_FET, w);
+    for (int i = tid; i < n; i += BLOCK) hist[i] = 0;
+    __syncthreads();
+    for (int rep = 0; rep < GD_NREP; ++rep) {
+      int got = 0;
+      while (got < n) {
+        const uint64_t xt = gd_affine_apply(jmp, xP);
+        const uint32_t r = gd_lcg_value(xt);
+        const int ok = r <= rd.limit;
+        int total;
+        const int incl = block_incl_scan<BLOCK>(ok, sh_scan, &total);
+        const int need = n - got;
+        const int rank = incl - 1;
+        if (ok && rank < need) {
+          const int j = got + rank;
+          const uint32_t v = gd_randint_mod(&rd, r);
+          if (nan_mode)
+            smp[n - 1 - j] = S[v];
+          else
+            atomicAdd(&hist[v], 1u);
+        }
+        if (total >= need) {
+          if (ok && rank == need - 1) sh_x = xt;
+          got = n;
+        } else {
+          if (tid == BLOCK - 1) sh_x = xt;
+          got += total;
+        }
+        __syncthreads();
+        xP = sh_x;
+        __syncthreads();
+      }
+      /* percentile of the replicate */
+      if (nan_mode) {
+        if (tid == 0) {
+          msort_glibc(smp, tmp, n);
+          sh_rep[rep] = gd_perc_mix(delta, smp[idx], smp[idx1]);
+        }
+        __syncthreads();
+      } else {
+        const int per = (n + BLOCK - 1) / BLOCK;
+        const int b0 = tid * per;
+        int local = 0;
+        for (int b = b0; b < b0 + per && b < n; ++b) local += (int)hist[b];
+        int total;
+        const int incl = block_incl_scan<BLOCK>(local, sh_scan, &total);
+        int cum = incl - local;
+        for (int b = b0; b < b0 + per && b < n; ++b) {
+          const int h = (int)hist[b];
+          if (cum <= idx && idx < cum + h) sh_pick[0] = b;
+          if (cum <= idx1 && idx1 < cum + h) sh_pick[1] = b;
+          cum += h;
+        }
+        __syncthreads();
+        for (int b = b0; b < b0 + per && b < n; ++b) hist[b] = 0;
+        if (tid == 0) sh_rep[rep] = gd_perc_mix(delta, S[sh_pick[0]], S[sh_pick[1]]);
+        __syncthreads();
+      }
+    }
+    if (tid == 0) {
+      double sd;
+      GD_STD_REVERSE(sd, sh_rep, GD_NREP);
+      scores[d.w_out + w] = wscore;
+      stddev[d.w_out + w] = sd;
+    }
+    __syncthreads();
+  }
+}
+
+template __global__ void k_fet_window_general<64, false>(const gd_chrom_dev *, int, const int32_t *,
+                                                         const unsigned *, int64_t, const int32_t *,
+                                                         const int32_t *, const int32_t *, const double *,
+                                                         const double *, const double *, const uint64_t *,
+                                                         double, double *, double *, unsigned *, int32_t *,
+                                                         unsigned *, double *, int64_t);
+template __global__ void k_fet_window_general<256, true>(const gd_chrom_dev *, int, const int32_t *,
+                                                         const unsigned *, int64_t, const int32_t *,
+                                                         const int32_t *, const int32_t *, const double *,
+                                                         const double *, const double *, const uint64_t *,
+                                                         double, double *, double *, unsigned *, int32_t *,
+                                                         unsigned *, double *, int64_t);

@@ -1,0 +1,36 @@
+/*
+ * gd_internal.h -- device-side descriptors shared by the kernels and the C-ABI glue.
+ *
+ * HBM layout of one scan (batch of chromosomes, all device-resident):
+ *   avals/bvals  f64  [sum alen] / [sum blen]   genotype values, SNP-major (as the
+ *   apos/bpos    i32  [sum alen] / [sum blen]   reference receives them), positions
+ *                                               repeated once per individual
+ *   lo_a/hi_a/lo_b i32 [sum wend]               window -> element index range
+ *   snp_score    f64  [sum alen]                per-SNP -log10 p, row s of chromosome
+ *                                               c at a_off(c) + s (rows <= alen)
+ *   scores/stddev f64 [sum regend/wstep]        caller-owned outputs
+ */
+#pragma once
+#include <stdint.h>
+
+typedef struct gd_chrom_dev {
+  int64_t a_off, b_off; /* element offsets into avals/apos and bvals/bpos */
+  int64_t w_base;       /* first global window index of this chromosome */
+  int64_t w_out;        /* output index of window 0 (scores/stddev/p) */
+  int32_t alen, blen;
+  int32_t regend, wend; /* windows [0, wend) are computed */
+  int32_t asize, bsize; /* get_population_size(), filled on the device */
+  int32_t nrows;        /* min(alen/asize, blen/bsize), filled on the device */
+  int32_t pad_;
+  uint64_t seed;
+} gd_chrom_dev;
+
+/* status bits raised by kernels into one device word */
+#define GD_FLAG_UNSORTED_A 1u
+#define GD_FLAG_UNSORTED_B 2u
+#define GD_FLAG_B_BOUNDS 4u
+#define GD_FLAG_BAD_SIZE 8u
+
+/* general-path window capacity held in LDS; larger windows use global scratch */
+#define GD_GEN_LDS_N 1024
+#define GD_NREP 100 /* bootstrap replicates (cFisher.c:62) */

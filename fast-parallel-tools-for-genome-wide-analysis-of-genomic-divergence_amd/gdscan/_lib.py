@@ -1,0 +1,102 @@
+"""ctypes binding of lib/libgdscan.so (the C ABI in include/gdscan.h).
+
+The library is the product: there is no Python or CPU fallback.  If it is
+missing or cannot be loaded this module raises at import time.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+PKG_DIR = Path(__file__).resolve().parent.parent
+LIB_DIR = PKG_DIR / "lib"
+LIB_PATH = LIB_DIR / "libgdscan.so"
+
+GD_OK = 0
+GD_ERR_ARG = -1
+GD_ERR_HIP = -2
+GD_ERR_UNSORTED = -4
+GD_ERR_BOUNDS = -5
+GD_ERR_SIZE = -6
+GD_DEFAULT_SEED = 20261015
+GD_WINDOWS_THREADED = 0
+GD_WINDOWS_SERIAL = 1
+GD_NSTAGES = 4
+
+# every symbol include/gdscan.h declares
+EXPORTS = (
+    "gd_fet_threadcompute", "gd_fet_compute", "gd_fet_scan_host",
+    "gd_css_threadcompute", "gd_css_compute", "gd_css_scan_host",
+    "gd_ctx_create", "gd_ctx_destroy", "gd_window_count",
+    "gd_fet_scan_device", "gd_css_scan_device",
+    "gd_set_seed", "gd_get_seed", "gd_last_error", "gd_device_count",
+    "gd_last_stage_ms", "gd_synth_device",
+)
+
+
+class GdError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"gdscan error {code}: {msg}")
+        self.code = code
+
+
+class Chrom(C.Structure):
+    _fields_ = [
+        ("a_off", C.c_int64), ("b_off", C.c_int64),
+        ("alen", C.c_int32), ("blen", C.c_int32),
+        ("regend", C.c_int32), ("pad_", C.c_int32),
+        ("w_out", C.c_int64), ("seed", C.c_uint64),
+    ]
+
+
+def _load() -> C.CDLL:
+    if not LIB_PATH.exists():
+        raise ImportError(
+            f"{LIB_PATH} is missing: build it with `make -C {PKG_DIR}` "
+            "(or __graft_entry__.build()); there is no fallback implementation")
+    lib = C.CDLL(str(LIB_PATH), mode=os.RTLD_NOW | getattr(os, "RTLD_GLOBAL", 0))
+    dp, ip, vp = C.POINTER(C.c_double), C.POINTER(C.c_int), C.c_void_p
+    i32 = C.c_int
+    fet_ref = [dp, dp, ip, ip, i32, i32, i32, i32, i32, i32, C.c_double, dp, dp]
+    css_ref = [dp, dp, ip, ip, i32, i32, i32, i32, i32, i32, i32, i32, i32, i32, dp, dp]
+    lib.gd_fet_threadcompute.argtypes = fet_ref
+    lib.gd_fet_compute.argtypes = fet_ref
+    lib.gd_fet_scan_host.argtypes = [dp, dp, ip, ip, i32, i32, i32, i32, i32, C.c_double, C.c_uint64, i32, dp, dp]
+    lib.gd_css_threadcompute.argtypes = css_ref
+    lib.gd_css_compute.argtypes = css_ref
+    lib.gd_css_scan_host.argtypes = [dp, dp, ip, ip, i32, i32, i32, i32, i32, i32, i32, C.c_uint64, i32, dp, dp]
+    lib.gd_ctx_create.argtypes = [i32]
+    lib.gd_ctx_create.restype = vp
+    lib.gd_ctx_destroy.argtypes = [vp]
+    lib.gd_ctx_destroy.restype = None
+    lib.gd_window_count.argtypes = [i32, i32, i32, i32]
+    lib.gd_fet_scan_device.argtypes = [vp, C.POINTER(Chrom), i32, vp, vp, vp, vp, i32, i32, C.c_double, i32,
+                                       vp, vp, vp]
+    lib.gd_css_scan_device.argtypes = [vp, C.POINTER(Chrom), i32, vp, vp, vp, vp, i32, i32, i32, i32, i32,
+                                       vp, vp, vp]
+    lib.gd_set_seed.argtypes = [C.c_uint64]
+    lib.gd_set_seed.restype = None
+    lib.gd_get_seed.restype = C.c_uint64
+    lib.gd_last_error.restype = C.c_char_p
+    lib.gd_last_stage_ms.argtypes = [C.POINTER(C.c_float), i32]
+    lib.gd_synth_device.argtypes = [i32, i32, i32, i32, C.c_uint64, vp, vp, vp, vp, vp, vp]
+    for fn in ("gd_fet_threadcompute", "gd_fet_compute", "gd_fet_scan_host", "gd_css_threadcompute",
+               "gd_css_compute", "gd_css_scan_host", "gd_fet_scan_device", "gd_css_scan_device",
+               "gd_synth_device", "gd_device_count", "gd_window_count", "gd_last_stage_ms"):
+        getattr(lib, fn).restype = C.c_int
+    return lib
+
+
+lib = _load()
+
+
+def check(code: int) -> None:
+    if code != GD_OK:
+        raise GdError(code, lib.gd_last_error().decode(errors="replace"))
+
+
+def last_stage_ms():
+    buf = (C.c_float * GD_NSTAGES)()
+    lib.gd_last_stage_ms(buf, GD_NSTAGES)
+    return list(buf)

@@ -1,0 +1,121 @@
+/*
+ * gdscan.h -- C ABI of the MI355X genomic-divergence window scanner (libgdscan.so).
+ *
+ * Drop-in boundary for the reference's hot path.  Each entry point names the
+ * reference interface it replaces (paths relative to the reference tree):
+ *
+ *   gd_fet_threadcompute  <- threadcompute()   statistics/fisher/threadfisher.h:33-34
+ *                            (bound by fisher_exact_tester, fisher_cython_parallel.pyx:14-15)
+ *   gd_fet_compute        <- compute()         statistics/fisher/cFisher.h:11-12
+ *                            (bound by fisher_exact_tester, fisher_cython.pyx:11-12)
+ *   gd_css_threadcompute  <- threadcompute()   statistics/css/threadcss.h:36-37
+ *                            (bound by cluster_separation_scorer, css_cython_parallel.pyx:14-15)
+ *   gd_css_compute        <- compute()         statistics/css/css.h:10-11
+ *
+ * The reference symbols are void and exit() on failure; ours return a status
+ * (GD_OK or a negative GD_ERR_*).  Buffers are caller-owned, plain host pointers,
+ * read-only except the outputs, which are written ONLY at the indices of windows
+ * the reference would compute (other entries keep the caller's values).  Calls are
+ * reentrant and thread-safe (a mutex per device context).
+ *
+ * Reproducibility: the reference seeds its bootstrap / permutation RNG from
+ * time(NULL); here every window w draws from its own nrand48 stream seeded by
+ * (seed, w) (gd_set_seed, default GD_DEFAULT_SEED), so stddev and p are
+ * deterministic.  Scores do not depend on the seed.
+ *
+ * libgdscan_fisher.so / libgdscan_css.so additionally export the reference's own
+ * names (threadcompute, compute) with the reference's exact signatures, so the
+ * unmodified .pyx files link against them.
+ */
+#ifndef GDSCAN_H
+#define GDSCAN_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GD_OK 0
+#define GD_ERR_ARG (-1)      /* invalid argument (wsize/wstep <= 0, perc outside [0,1], ...) */
+#define GD_ERR_HIP (-2)      /* HIP runtime failure (no device, out of memory, launch error) */
+#define GD_ERR_UNSORTED (-4) /* positions not non-decreasing (slide_right assumes sorted) */
+#define GD_ERR_BOUNDS (-5)   /* a window's B slice runs past blen (reference: out-of-bounds read) */
+#define GD_ERR_SIZE (-6)     /* empty population / unsupported window size */
+
+#define GD_DEFAULT_SEED 20261015ULL
+
+/* window set: which windows are computed */
+#define GD_WINDOWS_THREADED 0 /* threadcompute(): 100-window tasks, none if regend/wstep < 103 */
+#define GD_WINDOWS_SERIAL 1   /* compute(): every start with start + wsize <= regend + wstep */
+
+/* ---- FET: Fisher's exact test score (95th percentile of -log10 p) + bootstrap std ---- */
+int gd_fet_threadcompute(const double *avals, const double *bvals, const int *apos, const int *bpos, int regstart,
+                         int regend, int wsize, int wstep, int alen, int blen, double perc, double *scores,
+                         double *stddev);
+int gd_fet_compute(const double *avals, const double *bvals, const int *apos, const int *bpos, int regstart,
+                   int regend, int wsize, int wstep, int alen, int blen, double perc, double *scores,
+                   double *stddev);
+/* explicit seed and window set */
+int gd_fet_scan_host(const double *avals, const double *bvals, const int *apos, const int *bpos, int regend,
+                     int wsize, int wstep, int alen, int blen, double perc, uint64_t seed, int window_set,
+                     double *scores, double *stddev);
+
+/* ---- CSS: cluster separation score (classical MDS) + Monte-Carlo p ---- */
+int gd_css_threadcompute(const double *avals, const double *bvals, const int *apos, const int *bpos, int regstart,
+                         int regend, int wsize, int wstep, int alen, int blen, int treshold, int runs,
+                         int drosophila, int mds, double *scores, double *p);
+int gd_css_compute(const double *avals, const double *bvals, const int *apos, const int *bpos, int regstart,
+                   int regend, int wsize, int wstep, int alen, int blen, int treshold, int runs, int drosophila,
+                   int mds, double *scores, double *p);
+int gd_css_scan_host(const double *avals, const double *bvals, const int *apos, const int *bpos, int regend,
+                     int wsize, int wstep, int alen, int blen, int treshold, int runs, uint64_t seed,
+                     int window_set, double *scores, double *p);
+
+/* ---- device-resident batched scans (all pointers are device pointers except `chroms`) ---- */
+typedef struct gd_chrom {
+  int64_t a_off, b_off; /* element offsets of this chromosome in avals/apos and bvals/bpos */
+  int32_t alen, blen;   /* element counts */
+  int32_t regend;       /* region end (chromosome length); windows are [w*wstep, w*wstep+wsize] */
+  int32_t pad_;
+  int64_t w_out;        /* index in scores/stddev|p of this chromosome's window 0 */
+  uint64_t seed;        /* RNG seed of this chromosome's bootstrap / permutations */
+} gd_chrom;
+
+typedef struct gd_ctx gd_ctx;
+gd_ctx *gd_ctx_create(int device); /* NULL on failure */
+void gd_ctx_destroy(gd_ctx *ctx);
+
+/* Number of windows of one chromosome a scan writes: [0, n).  Pure arithmetic. */
+int gd_window_count(int regend, int wsize, int wstep, int window_set);
+
+int gd_fet_scan_device(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, const double *avals, const double *bvals,
+                       const int32_t *apos, const int32_t *bpos, int wsize, int wstep, double perc,
+                       int window_set, double *scores, double *stddev, void *hip_stream);
+
+int gd_css_scan_device(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, const double *avals, const double *bvals,
+                       const int32_t *apos, const int32_t *bpos, int wsize, int wstep, int treshold, int runs,
+                       int window_set, double *scores, double *p, void *hip_stream);
+
+/* ---- configuration / diagnostics ---- */
+void gd_set_seed(uint64_t seed);     /* seed used by the reference-signature entry points */
+uint64_t gd_get_seed(void);
+const char *gd_last_error(void);     /* thread-local message for the last failing call */
+int gd_device_count(void);
+
+/* kernel-level timing of the last device scan on this thread (ms, HIP events
+ * on the scan's stream), indexed by GD_STAGE_*; returns the number of stages */
+#define GD_STAGE_BOUNDS 0
+#define GD_STAGE_SNP 1
+#define GD_STAGE_WINDOW 2
+#define GD_STAGE_GENERAL 3
+#define GD_NSTAGES 4
+int gd_last_stage_ms(float *ms, int n);
+
+/* ---- synthetic tracks generated on the device (identical to gdscan/synth.py) ---- */
+int gd_synth_device(int chrom, int nsnp, int asize, int bsize, uint64_t seed, const double *freq_table,
+                    double *avals, double *bvals, int32_t *apos, int32_t *bpos, void *hip_stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,109 @@
+import ctypes
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+ROOT = Path(__file__).resolve().parent.parent
+PKG = ROOT / "fast-parallel-tools-for-genome-wide-analysis-of-genomic-divergence_amd"
+ORACLE_DIR = ROOT / "oracle"
+ORACLE_LIB = ORACLE_DIR / "_build" / "liboracle.so"
+REF_LIB = ORACLE_DIR / "_ref" / "libref_fisher.so"
+GOLDEN = ROOT / "tests" / "golden"
+
+if str(PKG) not in sys.path:
+    sys.path.insert(0, str(PKG))
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs through the HIP C-ABI)")
+
+
+def _gpu_available() -> bool:
+    try:
+        import torch
+        return torch.cuda.is_available()
+    except Exception:
+        return False
+
+
+def pytest_collection_modifyitems(config, items):
+    if _gpu_available():
+        return
+    skip = pytest.mark.skip(reason="no GPU in this environment")
+    for it in items:
+        if "gpu" in it.keywords:
+            it.add_marker(skip)
+
+
+DP = np.ctypeslib.ndpointer(np.float64, flags="C")
+IP = np.ctypeslib.ndpointer(np.int32, flags="C")
+
+
+@pytest.fixture(scope="session")
+def oracle():
+    """The CPU restatement (test infrastructure only)."""
+    if not ORACLE_LIB.exists():
+        subprocess.run(["make", "-C", str(ORACLE_DIR)], check=True, capture_output=True)
+    lib = ctypes.CDLL(str(ORACLE_LIB))
+    C = ctypes
+    lib.orc_fet_scan.argtypes = [DP, DP, IP, IP, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_double,
+                                 C.c_uint64, C.c_int, DP, DP]
+    lib.orc_fet.argtypes = [C.c_int] * 4
+    lib.orc_fet.restype = C.c_double
+    lib.orc_fet_p.argtypes = [C.c_int] * 4
+    lib.orc_fet_p.restype = C.c_double
+    lib.orc_fet_score.argtypes = [C.c_int] * 4
+    lib.orc_fet_score.restype = C.c_double
+    lib.orc_binomial.argtypes = [C.c_ulong, C.c_ulong]
+    lib.orc_binomial.restype = C.c_ulong
+    lib.orc_threaded_window_end.argtypes = [C.c_int] * 3
+    lib.orc_serial_window_end.argtypes = [C.c_int] * 3
+    lib.orc_window_state.argtypes = [C.c_uint64, C.c_uint64, C.c_long]
+    lib.orc_window_state.restype = C.c_uint64
+    lib.orc_nrand48_stream.argtypes = [C.c_uint64, C.c_int, np.ctypeslib.ndpointer(np.int64, flags="C")]
+    lib.orc_percentile.argtypes = [DP, C.c_int, C.c_double]
+    lib.orc_percentile.restype = C.c_double
+    lib.orc_population_size.argtypes = [IP, C.c_int]
+    return lib
+
+
+def oracle_fet_scan(orc, av, bv, ap, bp, regend, wsize=2500, wstep=500, perc=0.95, seed=20261015, serial=False):
+    n = regend // wstep
+    s = np.zeros(n)
+    d = np.zeros(n)
+    rc = orc.orc_fet_scan(av, bv, ap, bp, regend, wsize, wstep, len(av), len(bv), perc, seed, int(serial), s, d)
+    assert rc == 0
+    return s, d
+
+
+@pytest.fixture(scope="session")
+def refc():
+    """The reference's own FET C, compiled from /root/reference (dev container only)."""
+    if not REF_LIB.exists():
+        pytest.skip("oracle/_ref not built (needs /root/reference)")
+    lib = ctypes.CDLL(str(REF_LIB))
+    C = ctypes
+    lib.ref_fet_scan_seeded.argtypes = [DP, DP, IP, IP, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                        C.c_double, C.c_uint64, C.c_int, DP, DP]
+    lib.threadcompute.argtypes = [DP, DP, IP, IP] + [C.c_int] * 6 + [C.c_double, DP, DP]
+    lib.compute.argtypes = lib.threadcompute.argtypes
+    lib.fet.argtypes = [np.ctypeslib.ndpointer(np.int32, flags="C"), np.ctypeslib.ndpointer(np.int32, flags="C")]
+    lib.fet.restype = C.c_double
+    lib.fet_p.argtypes = [C.c_int] * 4
+    lib.fet_p.restype = C.c_double
+    lib.binomial.argtypes = [C.c_ulong, C.c_ulong]
+    lib.binomial.restype = C.c_ulong
+    return lib
+
+
+def close(a, b, rel=1e-9, abs_=1e-12):
+    """North-star tolerance: 1e-9 relative, with an absolute floor for near-zero stddev."""
+    a = np.asarray(a)
+    b = np.asarray(b)
+    both_nan = np.isnan(a) & np.isnan(b)
+    ok = both_nan | (np.abs(a - b) <= rel * np.maximum(np.abs(a), np.abs(b)) + abs_)
+    return bool(np.all(ok))

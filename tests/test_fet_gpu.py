@@ -1,0 +1,143 @@
+"""GPU parity: the HIP FET scan (through the C-ABI) against the oracle restatement.
+
+Tolerance (north star): 1e-9 relative.  Integer work (window bounds, counts, the
+nrand48 stream, order statistics) is exact; the only inexact step is -log10, which
+reproduces glibc's formula over a correctly rounded log (<= 1 ulp apart on ~0.1% of
+arguments), so scores are typically bit-identical and always within ~1e-15.
+"""
+import numpy as np
+import pytest
+
+from conftest import close, oracle_fet_scan
+
+pytestmark = pytest.mark.gpu
+
+
+def _synth(c, nsnp, a, b):
+    from gdscan import synth
+    return synth.chromosome(c, nsnp, a, b)
+
+
+@pytest.mark.parametrize("asize,bsize,nsnp", [(10, 10, 12000), (20, 20, 12000), (7, 13, 6000)])
+def test_threaded_scan_matches_oracle(oracle, asize, bsize, nsnp):
+    from gdscan import fet
+    av, bv, ap, bp, regend = _synth(1, nsnp, asize, bsize)
+    s_ref, d_ref = oracle_fet_scan(oracle, av, bv, ap, bp, regend)
+    s, d = fet.scan(av, bv, ap, bp, regend, seed=20261015)
+    assert (s_ref != 0).sum() > 100
+    assert close(s, s_ref) and close(d, d_ref)
+    # computed-window mask identical (zeros elsewhere)
+    assert np.array_equal(s_ref == 0, s == 0)
+    exact = np.mean(s == s_ref)
+    assert exact > 0.99, exact
+
+
+def test_serial_window_set(oracle):
+    from gdscan import fet
+    av, bv, ap, bp, regend = _synth(2, 3000, 10, 10)
+    s_ref, d_ref = oracle_fet_scan(oracle, av, bv, ap, bp, regend, serial=True)
+    s, d = fet.scan(av, bv, ap, bp, regend, seed=20261015, serial=True)
+    assert close(s, s_ref) and close(d, d_ref)
+
+
+@pytest.mark.parametrize("wsize,wstep", [(1000, 500), (5000, 500), (2000, 1000), (2500, 250)])
+def test_geometries(oracle, wsize, wstep):
+    from gdscan import fet
+    av, bv, ap, bp, regend = _synth(3, 8000, 10, 10)
+    s_ref, d_ref = oracle_fet_scan(oracle, av, bv, ap, bp, regend, wsize, wstep)
+    s, d = fet.scan(av, bv, ap, bp, regend, wsize, wstep, seed=20261015)
+    assert close(s, s_ref) and close(d, d_ref)
+
+
+def test_small_region_threaded_computes_nothing(oracle):
+    """Quirk Q3: regend/wstep - 3 < 100 -> the threaded driver runs no task."""
+    from gdscan import fet
+    av, bv, ap, bp, regend = _synth(4, 800, 10, 10)  # ~40 kb
+    s, d = fet.scan(av, bv, ap, bp, regend)
+    assert not s.any() and not d.any()
+    s2, d2 = fet.scan(av, bv, ap, bp, regend, serial=True)
+    s_ref, d_ref = oracle_fet_scan(oracle, av, bv, ap, bp, regend, serial=True)
+    assert s2.any() and close(s2, s_ref) and close(d2, d_ref)
+
+
+def test_reference_entry_point_in_place(oracle):
+    """fisher_exact_tester writes in place, leaves non-computed windows untouched."""
+    import fisher_cython_parallel as fcp
+    from gdscan import lib
+    av, bv, ap, bp, regend = _synth(5, 4000, 10, 10)
+    n = regend // 500
+    s = np.full(n, 7.0)
+    d = np.full(n, 7.0)
+    lib.gd_set_seed(99)
+    fcp.fisher_exact_tester(av, bv, ap, bp, 0, regend, 2500, 500, len(av), len(bv), 0.95, s, d)
+    s_ref = np.full(n, 7.0)
+    d_ref = np.full(n, 7.0)
+    oracle.orc_fet_scan(av, bv, ap, bp, regend, 2500, 500, len(av), len(bv), 0.95, 99, 0, s_ref, d_ref)
+    lib.gd_set_seed(20261015)
+    assert close(s, s_ref) and close(d, d_ref)
+    assert s[-1] == 7.0 and s[-3] == 7.0  # quirk Q2: last windows never computed
+
+
+def test_dtype_errors():
+    import fisher_cython_parallel as fcp
+    z = np.zeros(4)
+    with pytest.raises(ValueError):
+        fcp.fisher_exact_tester(np.zeros(4, np.float32), z, np.zeros(4, np.int32), np.zeros(4, np.int32), 0, 100,
+                                25, 5, 4, 4, 0.95, z, z)
+    with pytest.raises(ValueError):
+        fcp.fisher_exact_tester(z, z, np.zeros(4, np.int64), np.zeros(4, np.int32), 0, 100, 25, 5, 4, 4, 0.95,
+                                z, z)
+
+
+def test_unsorted_positions_rejected():
+    from gdscan import GdError, fet
+    av, bv, ap, bp, regend = _synth(6, 6000, 10, 10)
+    ap = ap.copy()
+    ap[5000:5010] = 1
+    with pytest.raises(GdError):
+        fet.scan(av, bv, ap, bp, regend)
+
+
+def test_misaligned_populations(oracle):
+    """B holds one extra leading SNP: every window's B slice starts on a different
+    row than A's -> per-window recomputation from the raw slices (general path)."""
+    from gdscan import fet
+    av, bv, ap, bp, regend = _synth(7, 6000, 10, 12)
+    bv2 = np.concatenate([np.full(12, 3.0), bv])
+    bp2 = np.concatenate([np.full(12, 0, np.int32), bp])
+    s_ref, d_ref = oracle_fet_scan(oracle, av, bv2, ap, bp2, regend)
+    s, d = fet.scan(av, bv2, ap, bp2, regend, seed=20261015)
+    assert close(s, s_ref) and close(d, d_ref)
+
+
+def test_dense_windows_global_scratch(oracle):
+    """npos > LDS capacity -> 256-thread workgroups with HBM scratch."""
+    from gdscan import fet
+    av, bv, ap, bp, regend = _synth(8, 20000, 4, 4)
+    # squeeze positions: 1 SNP per bp so a 2500-bp window holds ~2500 SNPs
+    ap = (ap // 50).astype(np.int32)
+    bp = (bp // 50).astype(np.int32)
+    regend = int(ap[-1]) + 1
+    s_ref, d_ref = oracle_fet_scan(oracle, av, bv, ap, bp, regend, 2500, 100)
+    s, d = fet.scan(av, bv, ap, bp, regend, 2500, 100, seed=20261015)
+    assert (s_ref != 0).sum() > 50
+    assert close(s, s_ref) and close(d, d_ref)
+
+
+def test_large_cohort_overflow_semantics(oracle):
+    """40+40: binomial() overflow to 0 (first at C(68,31)) gives inf/NaN p for some
+    SNPs; NaN windows use glibc's merge-sort order on the GPU too."""
+    from gdscan import fet
+    av, bv, ap, bp, regend = _synth(9, 6000, 40, 40)
+    s_ref, d_ref = oracle_fet_scan(oracle, av, bv, ap, bp, regend)
+    s, d = fet.scan(av, bv, ap, bp, regend, seed=20261015)
+    assert close(s, s_ref) and close(d, d_ref)
+
+
+def test_percentiles(oracle):
+    from gdscan import fet
+    av, bv, ap, bp, regend = _synth(10, 6000, 10, 10)
+    for perc in (0.0, 0.5, 0.8, 1.0):
+        s_ref, d_ref = oracle_fet_scan(oracle, av, bv, ap, bp, regend, perc=perc)
+        s, d = fet.scan(av, bv, ap, bp, regend, perc=perc, seed=20261015)
+        assert close(s, s_ref) and close(d, d_ref), perc
