@@ -1,0 +1,236 @@
+#!/usr/bin/env python3
+"""Benchmark: genome-wide FET window scan on MI355X (BASELINE.json configs[1]).
+
+One step = one device-resident FET scan (per-SNP Fisher exact test, window
+95th-percentile score, 100-replicate bootstrap stddev) over this rank's batch of
+synthetic chromosomes: 20 chromosomes x 500k SNPs, 20+20 individuals, 2.5 kb
+windows / 500 bp step  (10M SNPs, ~1M windows per GPU).  Inputs are generated on
+the device before timing; weak scaling: every rank scans its own 20 chromosomes
+(chromosome ids rank*20 .. rank*20+19), no data-path collective.
+
+Prints ONE JSON line (rank 0).  `roofline` prices the whole scan's algorithmic
+HBM bytes B = 12*(alen+blen) + 16*W (f64 value + i32 position per
+genotype, two f64 outputs per window) against its kernel time, and also lists each
+stage's kernel time.  `cpu_baseline` times the reference's own Pthreads threadcompute()
+(oracle/_ref, compiled from the reference sources) on a bounded sample of the same
+workload, or the oracle port when that binary is absent.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+PKG = ROOT / "fast-parallel-tools-for-genome-wide-analysis-of-genomic-divergence_amd"
+sys.path.insert(0, str(PKG))
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, HBM3E spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--nchrom", type=int, default=20)
+    ap.add_argument("--nsnp", type=int, default=500_000)
+    ap.add_argument("--asize", type=int, default=20)
+    ap.add_argument("--bsize", type=int, default=20)
+    ap.add_argument("--wsize", type=int, default=2500)
+    ap.add_argument("--wstep", type=int, default=500)
+    ap.add_argument("--perc", type=float, default=0.95)
+    ap.add_argument("--cpu-chroms", type=int, default=20, help="chromosomes in the CPU-baseline sample")
+    ap.add_argument("--no-cpu", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_baseline(args):
+    """Reference threadcompute() (64 pthreads) on a sample of the same workload."""
+    from gdscan import synth
+
+    ref = ROOT / "oracle" / "_ref" / "libref_fisher.so"
+    orc = ROOT / "oracle" / "_build" / "liboracle.so"
+    DP = np.ctypeslib.ndpointer(np.float64, flags="C")
+    IP = np.ctypeslib.ndpointer(np.int32, flags="C")
+    C = ctypes
+    if ref.exists():
+        lib = C.CDLL(str(ref))
+        fn = lib.threadcompute
+        fn.argtypes = [DP, DP, IP, IP] + [C.c_int] * 6 + [C.c_double, DP, DP]
+        kind, cores = "reference", 64
+    else:
+        lib = C.CDLL(str(orc))
+        fn = lib.orc_fet_scan
+        fn.argtypes = [DP, DP, IP, IP, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_double, C.c_uint64,
+                       C.c_int, DP, DP]
+        kind, cores = "port", 1
+    total_w = 0
+    total_t = 0.0
+    for c in range(args.cpu_chroms):
+        av, bv, ap_, bp, regend = synth.chromosome(c, args.nsnp, args.asize, args.bsize)
+        n = regend // args.wstep
+        s = np.zeros(n)
+        d = np.zeros(n)
+        # the reference prints progress on C stdout: silence it around the call
+        sys.stdout.flush()
+        saved = os.dup(1)
+        devnull = os.open(os.devnull, os.O_WRONLY)
+        os.dup2(devnull, 1)
+        try:
+            t0 = time.perf_counter()
+            if kind == "reference":
+                fn(av, bv, ap_, bp, 0, regend, args.wsize, args.wstep, len(av), len(bv), args.perc, s, d)
+            else:
+                fn(av, bv, ap_, bp, regend, args.wsize, args.wstep, len(av), len(bv), args.perc, 1, 0, s, d)
+            total_t += time.perf_counter() - t0
+        finally:
+            os.dup2(saved, 1)
+            os.close(saved)
+            os.close(devnull)
+        from gdscan import fet
+        total_w += fet.window_count(regend, args.wsize, args.wstep)
+    return {
+        "value": total_w / total_t,
+        "unit": "windows/s",
+        "cores": cores,
+        "kind": kind,
+        "sample": f"{args.cpu_chroms} of the {args.nchrom} chromosomes ({args.nsnp} SNPs, "
+                  f"{args.asize}+{args.bsize}), {total_w} windows in {total_t:.2f} s"
+                  + (" with the reference's 64 pthreads" if kind == "reference" else ", 1 thread"),
+    }
+
+
+def main():
+    args = parse()
+    import torch
+
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local = int(os.environ.get("LOCAL_RANK", 0))
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist_mod
+        dist_mod.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dist = dist_mod
+
+    from gdscan import _lib, synth
+    from gdscan._lib import Chrom, check, lib
+
+    dev = torch.device("cuda", local)
+    a, b, nsnp, nch = args.asize, args.bsize, args.nsnp, args.nchrom
+    alen, blen = nsnp * a, nsnp * b
+    avals = torch.empty(nch * alen, dtype=torch.float64, device=dev)
+    bvals = torch.empty(nch * blen, dtype=torch.float64, device=dev)
+    apos = torch.empty(nch * alen, dtype=torch.int32, device=dev)
+    bpos = torch.empty(nch * blen, dtype=torch.int32, device=dev)
+    qtab = torch.from_numpy(synth.freq_table()).to(dev)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    for c in range(nch):
+        gc = rank * nch + c
+        check(lib.gd_synth_device(gc, nsnp, a, b, synth.MASTER_SEED, qtab.data_ptr(),
+                                  avals.data_ptr() + c * alen * 8, bvals.data_ptr() + c * blen * 8,
+                                  apos.data_ptr() + c * alen * 4, bpos.data_ptr() + c * blen * 4, stream))
+    torch.cuda.synchronize()
+    # regend of each chromosome = last position + 1
+    last = apos.view(nch, alen)[:, -1].cpu().numpy().astype(np.int64)
+    chroms = (Chrom * nch)()
+    w_out = 0
+    windows = 0
+    for c in range(nch):
+        regend = int(last[c]) + 1
+        chroms[c].a_off = c * alen
+        chroms[c].b_off = c * blen
+        chroms[c].alen = alen
+        chroms[c].blen = blen
+        chroms[c].regend = regend
+        chroms[c].w_out = w_out
+        chroms[c].seed = synth.MASTER_SEED + rank * nch + c
+        w_out += regend // args.wstep
+        windows += lib.gd_window_count(regend, args.wsize, args.wstep, _lib.GD_WINDOWS_THREADED)
+    scores = torch.zeros(w_out, dtype=torch.float64, device=dev)
+    stddev = torch.zeros(w_out, dtype=torch.float64, device=dev)
+    ctx = lib.gd_ctx_create(local)
+    assert ctx, "gd_ctx_create failed"
+
+    def step():
+        check(lib.gd_fet_scan_device(ctx, chroms, nch, avals.data_ptr(), bvals.data_ptr(), apos.data_ptr(),
+                                     bpos.data_ptr(), args.wsize, args.wstep, args.perc,
+                                     _lib.GD_WINDOWS_THREADED, scores.data_ptr(), stddev.data_ptr(), stream))
+
+    for _ in range(args.warmup):
+        step()
+    stage = np.zeros(_lib.GD_NSTAGES)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+        stage += np.array(_lib.last_stage_ms())
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    stage /= args.steps
+    ms_per_step = elapsed * 1e3 / args.steps
+    total_windows = windows * world
+    value = total_windows * args.steps / elapsed
+
+    kernel_ms = float(stage.sum())
+    alg_bytes = 12.0 * (nch * (alen + blen)) + 16.0 * windows
+    achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
+    out = {
+        "metric": "FET genomic windows/sec (10M SNPs, 20+20 indiv, 2.5 kb windows; per-GPU batch)",
+        "value": value,
+        "unit": "windows/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (seeded generator, SURVEY.md 8(d)), generated on device",
+        "config": {
+            "workload": "FET genome-wide, configs[1]: 20 chromosomes x 500k SNPs per GPU, 20+20 individuals, "
+                        "wsize 2500, wstep 500, perc 0.95, 100 bootstrap replicates",
+            "chromosomes_per_gpu": nch, "snps_per_gpu": nch * nsnp, "windows_per_gpu": windows,
+            "asize": a, "bsize": b, "parallelism": f"window-sharded x{world} (whole chromosomes per rank)",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS,
+            "traffic": None,
+            "kernel": "whole scan (bounds + per-SNP FET + window bootstrap), HIP events per step",
+            "alg_bytes_per_step": alg_bytes,
+            "stage_ms": {"bounds": stage[0], "snp_fet": stage[1], "window_fast": stage[2],
+                         "window_general": stage[3]},
+        },
+    }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        out["cpu_baseline"] = cpu_baseline(args)
+    lib.gd_ctx_destroy(ctx)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

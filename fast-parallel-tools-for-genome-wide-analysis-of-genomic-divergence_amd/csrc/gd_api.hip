@@ -279,7 +279,7 @@ static int fet_scan_locked(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, cons
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipEventRecord(ctx->ev[1], s));
   {
-    const unsigned gx = (unsigned)std::min<int64_t>((pl.max_alen + 255) / 256, 4096);
+    const unsigned gx = (unsigned)std::min<int64_t>((pl.max_alen + 255) / 256, std::max(1, 8192 / nchrom));
     hipLaunchKernelGGL(k_snp_fet, dim3(std::max(gx, 1u), nchrom), dim3(256), 0, s, d_ch, avals, bvals,
                        ctx->binom, snp);
   }

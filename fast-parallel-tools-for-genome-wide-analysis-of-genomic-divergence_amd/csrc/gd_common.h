@@ -124,10 +124,10 @@ GD_HD gd_randint gd_randint_make(uint32_t n) {
   return d;
 }
 
+/* branch-free: for n == 1 the magic is 0 (q = 0) and the result is masked to 0 */
 GD_HD uint32_t gd_randint_mod(const gd_randint *d, uint32_t r) {
-  if (d->n == 1) return 0;
-  uint32_t q = (uint32_t)(((uint64_t)r * d->magic) >> 32) >> d->shift;
-  return r - q * d->n;
+  const uint32_t q = (uint32_t)(((uint64_t)r * d->magic) >> 32) >> d->shift;
+  return (r - q * d->n) & (d->n == 1 ? 0u : 0xFFFFFFFFu);
 }
 
 /* ------------------------------------------------------------------------- */

@@ -144,8 +144,20 @@ __global__ void __launch_bounds__(64) k_popsize(gd_chrom_dev *ch, const int32_t 
   }
 }
 
+/* floor(a / b) for b > 0, |a| < 2^40: double-reciprocal estimate, one fix-up step */
+__device__ __forceinline__ int64_t fdiv_fast(int64_t a, int32_t b, double inv) {
+  int64_t q = (int64_t)floor((double)a * inv);
+  const int64_t r = a - q * (int64_t)b;
+  q += (r >= b) - (r < 0);
+  return q;
+}
+
 /* slide_right() for all windows: lo = first idx with pos >= start,
- * hi = first idx with pos > start + wsize (inclusive end).  Grid (x, chrom, pop). */
+ * hi = first idx with pos > start + wsize (inclusive end).  Grid (x, chrom, pop).
+ * Element i owns the windows whose start lies in (pos[i-1], pos[i]] (lo) and whose
+ * inclusive stop lies in [pos[i-1], pos[i]) (hi); i == len is the +inf sentinel.
+ * Within a SNP's run of identical positions nothing is owned, so the common case
+ * is one compare; each thread takes 4 consecutive elements. */
 __global__ void __launch_bounds__(256) k_bounds(const gd_chrom_dev *ch, const int32_t *apos, const int32_t *bpos,
                                                 int wsize, int wstep, int32_t *lo_a, int32_t *hi_a,
                                                 int32_t *lo_b, unsigned *flags) {
@@ -157,37 +169,130 @@ __global__ void __launch_bounds__(256) k_bounds(const gd_chrom_dev *ch, const in
   const int32_t *pos = pop ? bpos + d.b_off : apos + d.a_off;
   int32_t *lo = (pop ? lo_b : lo_a) + d.w_base;
   int32_t *hi = hi_a + d.w_base;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= len; i += stride) {
-    const int64_t p = (i < len) ? pos[i] : 0;
-    const int64_t pp = (i > 0) ? pos[i - 1] : 0;
-    if (i > 0 && i < len && p < pp) atomicOr(flags, pop ? GD_FLAG_UNSORTED_B : GD_FLAG_UNSORTED_A);
-    int64_t f = (i == 0) ? 0 : fdiv(pp, wstep) + 1;
-    int64_t l = (i == len) ? wend - 1 : fdiv(p, wstep);
-    if (f < 0) f = 0;
-    if (l > wend - 1) l = wend - 1;
-    for (int64_t w = f; w <= l; ++w) lo[w] = (int32_t)i;
-    if (pop == 0) {
-      f = (i == 0) ? 0 : cdiv(pp - wsize, wstep);
-      l = (i == len) ? wend - 1 : cdiv(p - wsize, wstep) - 1;
+  const double inv = 1.0 / (double)wstep;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x * 4;
+  bool unsorted = false;
+  for (int64_t i0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4; i0 <= len; i0 += stride) {
+    int32_t v[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+      const int64_t i = i0 - 1 + k;
+      v[k] = (i >= 0 && i < len) ? pos[i] : 0;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int64_t i = i0 + k;
+      if (i > len) break;
+      const bool first = (i == 0), last = (i == len);
+      const int64_t p = v[k + 1], pp = v[k];
+      if (!first && !last) {
+        if (p == pp) continue;
+        unsorted |= (p < pp);
+      }
+      int64_t f = first ? 0 : fdiv_fast(pp, wstep, inv) + 1;
+      int64_t l = last ? wend - 1 : fdiv_fast(p, wstep, inv);
       if (f < 0) f = 0;
       if (l > wend - 1) l = wend - 1;
-      for (int64_t w = f; w <= l; ++w) hi[w] = (int32_t)i;
+      for (int64_t w = f; w <= l; ++w) lo[w] = (int32_t)i;
+      if (pop == 0) {
+        f = first ? 0 : -fdiv_fast(wsize - pp, wstep, inv);
+        l = last ? wend - 1 : -fdiv_fast(wsize - p, wstep, inv) - 1;
+        if (f < 0) f = 0;
+        if (l > wend - 1) l = wend - 1;
+        for (int64_t w = f; w <= l; ++w) hi[w] = (int32_t)i;
+      }
     }
   }
+  if (unsorted) atomicOr(flags, pop ? GD_FLAG_UNSORTED_B : GD_FLAG_UNSORTED_A);
 }
 
-/* one thread per SNP row: counts -> Zar two-tailed p -> -log10 */
+/* ------------------------------------------------------------------------ */
+/* Per-SNP FET.  A workgroup takes a tile of R SNP rows.  Its four waves stream   */
+/* the tile's genotype values with coalesced 16-byte loads (two values per lane,  */
+/* 128 per wave-instruction) and turn them into ballot bit masks of "== 3" and     */
+/* "== -3" (even / odd element of each lane separately), kept in LDS.  Thread r   */
+/* then counts its row's bits with popcounts, runs the Zar two-tailed test and     */
+/* -log10.  Values are read once from HBM at full width; the FP compare is the     */
+/* reference's exact double compare (fetcount, cFisher.c:216-233).               */
+/* ------------------------------------------------------------------------ */
+#define SF_MAXCH 168 /* 128-element chunks per population per tile */
+
+namespace {
+
+__device__ __forceinline__ uint64_t lane_range(int a, int b) {
+  const uint64_t hi = (b >= 64) ? ~0ull : ((1ull << b) - 1);
+  const uint64_t lo = (a >= 64) ? ~0ull : ((1ull << a) - 1);
+  return hi & ~lo;
+}
+
+/* bits set among tile-relative elements [s, e) of one (pop, kind) mask set */
+__device__ __forceinline__ int count_range(const uint64_t (*m)[2], int s, int e) {
+  int cnt = 0;
+  for (int k = s >> 7; k <= (e - 1) >> 7; ++k) {
+    const int ls = max(s - (k << 7), 0), le = min(e - (k << 7), 128);
+    cnt += __popcll(m[k][0] & lane_range((ls + 1) >> 1, (le + 1) >> 1)) +
+           __popcll(m[k][1] & lane_range(ls >> 1, le >> 1));
+  }
+  return cnt;
+}
+
+}  // namespace
+
 __global__ void __launch_bounds__(256) k_snp_fet(const gd_chrom_dev *ch, const double *avals, const double *bvals,
                                                  const uint64_t *binom, double *snp_score) {
+  __shared__ uint64_t sh_m[2][2][SF_MAXCH][2]; /* [pop][maj/min][chunk][even/odd] */
   const gd_chrom_dev &d = ch[blockIdx.y];
-  const int nrows = d.nrows, asize = d.asize, bsize = d.bsize;
   if (d.wend <= 0) return;
-  const double *a = avals + d.a_off;
-  const double *b = bvals + d.b_off;
-  double *out = snp_score + d.a_off;
-  for (int s = blockIdx.x * blockDim.x + threadIdx.x; s < nrows; s += gridDim.x * blockDim.x)
-    out[s] = snp_score_raw(a + (int64_t)s * asize, asize, b + (int64_t)s * bsize, bsize, binom);
+  const int nrows = d.nrows, asize = d.asize, bsize = d.bsize;
+  const int big = max(asize, bsize);
+  const int R = min(256, ((SF_MAXCH - 2) * 128) / max(big, 1));
+  if (R <= 0 || nrows <= 0) return;
+  const int ntiles = (nrows + R - 1) / R;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int s0 = tile * R;
+    const int rows = min(R, nrows - s0);
+    int rel0[2];
+    for (int pop = 0; pop < 2; ++pop) {
+      const int size = pop ? bsize : asize;
+      const double *vals = pop ? bvals : avals;
+      const int64_t start = (pop ? d.b_off : d.a_off) + (int64_t)s0 * size;
+      const int64_t stop = start + (int64_t)rows * size;
+      const int64_t gb = start & ~(int64_t)1; /* 16-byte aligned element */
+      rel0[pop] = (int)(start - gb);
+      const int nch = (int)((stop - gb + 127) >> 7);
+      for (int k = wave; k < nch; k += 4) {
+        const int64_t e = gb + ((int64_t)k << 7) + 2 * lane;
+        double v0 = 0.0, v1 = 0.0;
+        if (e + 1 < stop) {
+          const double2 t = *reinterpret_cast<const double2 *>(vals + e);
+          v0 = t.x;
+          v1 = t.y;
+        } else if (e < stop) {
+          v0 = vals[e];
+        }
+        const uint64_t ja = __ballot(v0 == 3.0), jb = __ballot(v1 == 3.0);
+        const uint64_t na = __ballot(v0 == -3.0), nb = __ballot(v1 == -3.0);
+        if (lane == 0) {
+          sh_m[pop][0][k][0] = ja;
+          sh_m[pop][0][k][1] = jb;
+          sh_m[pop][1][k][0] = na;
+          sh_m[pop][1][k][1] = nb;
+        }
+      }
+    }
+    __syncthreads();
+    const int r = threadIdx.x;
+    if (r < rows) {
+      const int sa = rel0[0] + r * asize, sb = rel0[1] + r * bsize;
+      const int f0 = count_range(sh_m[0][0], sa, sa + asize);
+      const int f1 = count_range(sh_m[0][1], sa, sa + asize);
+      const int f2 = count_range(sh_m[1][0], sb, sb + bsize);
+      const int f3 = count_range(sh_m[1][1], sb, sb + bsize);
+      snp_score[d.a_off + s0 + r] = gd_fet_score_from_p(fet_p_two_tailed(f0, f1, f2, f3, binom));
+    }
+    __syncthreads();
+  }
 }
 
 /* ------------------------------------------------------------------------ */

@@ -141,3 +141,65 @@ def test_percentiles(oracle):
         s_ref, d_ref = oracle_fet_scan(oracle, av, bv, ap, bp, regend, perc=perc)
         s, d = fet.scan(av, bv, ap, bp, regend, perc=perc, seed=20261015)
         assert close(s, s_ref) and close(d, d_ref), perc
+
+
+def test_device_synth_matches_numpy():
+    import torch
+    from gdscan import synth
+    from gdscan._lib import check, lib
+    nsnp, a, b = 3000, 5, 7
+    av, bv, ap, bp, regend = synth.chromosome(11, nsnp, a, b)
+    dev = torch.device("cuda", 0)
+    t = [torch.empty(nsnp * a, dtype=torch.float64, device=dev), torch.empty(nsnp * b, dtype=torch.float64, device=dev),
+         torch.empty(nsnp * a, dtype=torch.int32, device=dev), torch.empty(nsnp * b, dtype=torch.int32, device=dev)]
+    q = torch.from_numpy(synth.freq_table()).to(dev)
+    check(lib.gd_synth_device(11, nsnp, a, b, synth.MASTER_SEED, q.data_ptr(), *[x.data_ptr() for x in t],
+                              torch.cuda.current_stream().cuda_stream))
+    torch.cuda.synchronize()
+    for x, y in zip(t, (av, bv, ap, bp)):
+        assert np.array_equal(x.cpu().numpy(), y)
+
+
+def test_device_batch_api_matches_host(oracle):
+    """Several chromosomes in one device scan == per-chromosome scans."""
+    import torch
+    from gdscan import _lib, synth
+    from gdscan._lib import Chrom, check, lib
+    dev = torch.device("cuda", 0)
+    data = [synth.chromosome(20 + c, n, 10, 10) for c, n in enumerate((5000, 7000, 600, 6000))]
+    A = np.concatenate([x[0] for x in data]); B = np.concatenate([x[1] for x in data])
+    AP = np.concatenate([x[2] for x in data]); BP = np.concatenate([x[3] for x in data])
+    chroms = (Chrom * len(data))()
+    off_a = off_b = w = 0
+    for i, (av, bv, ap, bp, regend) in enumerate(data):
+        chroms[i].a_off, chroms[i].b_off, chroms[i].alen, chroms[i].blen = off_a, off_b, len(av), len(bv)
+        chroms[i].regend, chroms[i].w_out, chroms[i].seed = regend, w, 1000 + i
+        off_a += len(av); off_b += len(bv); w += regend // 500
+    tens = [torch.from_numpy(x).to(dev) for x in (A, B, AP, BP)]
+    sc = torch.zeros(w, dtype=torch.float64, device=dev); sd = torch.zeros_like(sc)
+    ctx = lib.gd_ctx_create(0)
+    check(lib.gd_fet_scan_device(ctx, chroms, len(data), *[t.data_ptr() for t in tens], 2500, 500, 0.95,
+                                 _lib.GD_WINDOWS_THREADED, sc.data_ptr(), sd.data_ptr(),
+                                 torch.cuda.current_stream().cuda_stream))
+    lib.gd_ctx_destroy(ctx)
+    sc = sc.cpu().numpy(); sd = sd.cpu().numpy()
+    w = 0
+    for i, (av, bv, ap, bp, regend) in enumerate(data):
+        s_ref, d_ref = oracle_fet_scan(oracle, av, bv, ap, bp, regend, seed=1000 + i)
+        n = regend // 500
+        assert close(sc[w:w + n], s_ref) and close(sd[w:w + n], d_ref), i
+        w += n
+
+
+def test_fast_path_equals_literal_path_full_chromosome(monkeypatch):
+    """Size-independent property at full chromosome scale (500k SNPs, 20+20, ~50k
+    windows): the register order-statistic bootstrap equals the literal
+    sort-and-histogram path bit for bit."""
+    from gdscan import fet
+    av, bv, ap, bp, regend = _synth(0, 500_000, 20, 20)
+    s_fast, d_fast = fet.scan(av, bv, ap, bp, regend, seed=5)
+    monkeypatch.setenv("GD_FORCE_GENERAL", "1")
+    s_lit, d_lit = fet.scan(av, bv, ap, bp, regend, seed=5)
+    monkeypatch.delenv("GD_FORCE_GENERAL")
+    assert (s_fast != 0).sum() > 49_000
+    assert np.array_equal(s_fast, s_lit) and np.array_equal(d_fast, d_lit)

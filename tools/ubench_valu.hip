@@ -1,0 +1,64 @@
+// Microbenchmark: VALU throughput of the ops an nrand48 bootstrap loop can use
+// (gfx950).  Exact instructions via inline asm, 8 independent chains per lane.
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#define N_IT 2048
+#define CH 8
+template <int OP>
+__global__ void k(unsigned *out, unsigned seed) {
+  unsigned a[CH];
+  double d[CH];
+  const unsigned c = seed * 0x9E3779B9u | 1u;
+  const double cd = 1.0000001;
+  for (int i = 0; i < CH; ++i) { a[i] = seed + threadIdx.x * 7 + i; d[i] = a[i]; }
+  for (int it = 0; it < N_IT; ++it) {
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+      if (OP == 0) asm volatile("v_add_u32 %0, %0, %1" : "+v"(a[i]) : "v"(c));
+      if (OP == 1) asm volatile("v_mul_lo_u32 %0, %0, %1" : "+v"(a[i]) : "v"(c));
+      if (OP == 2) asm volatile("v_mul_hi_u32 %0, %0, %1" : "+v"(a[i]) : "v"(c));
+      if (OP == 3) asm volatile("v_mul_u32_u24 %0, %0, %1" : "+v"(a[i]) : "v"(c));
+      if (OP == 4) asm volatile("v_fma_f64 %0, %0, %1, %1" : "+v"(d[i]) : "v"(cd));
+      if (OP == 5) asm volatile("v_med3_i32 %0, %0, %1, %1" : "+v"(a[i]) : "v"(c));
+      if (OP == 6) asm volatile("v_mul_f64 %0, %0, %1" : "+v"(d[i]) : "v"(cd));
+      if (OP == 7) asm volatile("v_mul_hi_u32_u24 %0, %0, %1" : "+v"(a[i]) : "v"(c));
+      if (OP == 8) asm volatile("v_alignbit_b32 %0, %0, %1, 17" : "+v"(a[i]) : "v"(c));
+      if (OP == 9) asm volatile("v_floor_f64 %0, %0" : "+v"(d[i]));
+      if (OP == 10) asm volatile("v_cvt_f64_u32 %0, %1" : "=v"(d[i]) : "v"(a[i]));
+    }
+  }
+  unsigned s = 0;
+  for (int i = 0; i < CH; ++i) s += a[i] + (unsigned)d[i];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+template <int OP>
+float run(unsigned *o) {
+  hipEvent_t e0, e1;
+  (void)hipEventCreate(&e0);
+  (void)hipEventCreate(&e1);
+  hipLaunchKernelGGL(k<OP>, dim3(256 * 8), dim3(256), 0, 0, o, 1u);
+  (void)hipEventRecord(e0);
+  for (int r = 0; r < 5; ++r) hipLaunchKernelGGL(k<OP>, dim3(256 * 8), dim3(256), 0, 0, o, 1u);
+  (void)hipEventRecord(e1);
+  (void)hipEventSynchronize(e1);
+  float ms;
+  (void)hipEventElapsedTime(&ms, e0, e1);
+  double ops = 5.0 * 256 * 8 * 256 * (double)N_IT * CH;
+  return (float)(ops / (ms * 1e-3) / 1e12);
+}
+int main() {
+  unsigned *o;
+  (void)hipMalloc(&o, 256 * 8 * 256 * 4);
+  printf("v_add_u32        %.1f Tlane-op/s\n", run<0>(o));
+  printf("v_mul_lo_u32     %.1f\n", run<1>(o));
+  printf("v_mul_hi_u32     %.1f\n", run<2>(o));
+  printf("v_mul_u32_u24    %.1f\n", run<3>(o));
+  printf("v_fma_f64        %.1f\n", run<4>(o));
+  printf("v_med3_i32       %.1f\n", run<5>(o));
+  printf("v_mul_f64        %.1f\n", run<6>(o));
+  printf("v_mul_hi_u32_u24 %.1f\n", run<7>(o));
+  printf("v_alignbit_b32   %.1f\n", run<8>(o));
+  printf("v_floor_f64      %.1f\n", run<9>(o));
+  printf("v_cvt_f64_u32    %.1f\n", run<10>(o));
+  return 0;
+}
