@@ -29,7 +29,10 @@ __global__ void k_popsize(gd_chrom_dev *ch, const int32_t *apos, const int32_t *
 __global__ void k_bounds(const gd_chrom_dev *ch, const int32_t *apos, const int32_t *bpos, int wsize, int wstep,
                          int32_t *lo_a, int32_t *hi_a, int32_t *lo_b, unsigned *flags);
 __global__ void k_snp_fet(const gd_chrom_dev *ch, const double *avals, const double *bvals, const uint64_t *binom,
-                          double *snp_score);
+                          const int *lut_hdr, const double *lut, double *snp_score);
+__global__ void k_fet_lut_build(const gd_chrom_dev *ch, const uint64_t *binom, const int *hdr, double *lut,
+                                int64_t cap);
+__global__ void k_fet_lut_publish(const gd_chrom_dev *ch, int *hdr, int64_t cap);
 template <int BLOCK, bool GLOBAL_SCRATCH>
 __global__ void k_fet_window_general(const gd_chrom_dev *ch, int nchrom, const int32_t *wlist,
                                      const unsigned *wlist_count, int64_t wtotal, const int32_t *lo_a,
@@ -38,10 +41,13 @@ __global__ void k_fet_window_general(const gd_chrom_dev *ch, int nchrom, const i
                                      double perc, double *scores, double *stddev, unsigned *flags,
                                      int32_t *huge_list, unsigned *huge_count, double *gscratch,
                                      int64_t gscratch_n);
-int gd_fet_window_fast_launch(const gd_chrom_dev *ch, int nchrom, int64_t wtotal, const int32_t *lo_a,
-                              const int32_t *hi_a, const int32_t *lo_b, const double *snp_score, double perc,
-                              double *scores, double *stddev, unsigned *flags, int32_t *slow_list,
-                              unsigned *slow_count, hipStream_t s);
+int gd_fet_fast_windows_per_block();
+int gd_fet_window_prepare(int64_t wtotal, int32_t *slow_list, unsigned *slow_count, hipStream_t s,
+                          bool *force_general);
+int gd_fet_window_fast_launch(const gd_chrom_dev *ch, int nchrom, const int32_t *blk_off, int blk_begin,
+                              int blk_count, const int32_t *lo_a, const int32_t *hi_a, const int32_t *lo_b,
+                              const double *snp_score, double perc, double *scores, double *stddev,
+                              unsigned *flags, int32_t *slow_list, unsigned *slow_count, hipStream_t s);
 int gd_css_pipeline(struct gd_ctx *ctx, const gd_chrom_dev *d_ch, const std::vector<gd_chrom_dev> &h_ch,
                     int64_t wtotal, const double *avals, const double *bvals, int wsize, int wstep, int treshold,
                     int runs, double *scores, double *p, hipStream_t s);
@@ -68,12 +74,17 @@ static int fail(int code, const std::string &msg) {
 struct gd_ctx {
   int device = 0;
   std::mutex mu;
-  hipStream_t stream = nullptr; /* used by the host entry points */
+  hipStream_t stream = nullptr;  /* used by the host entry points */
+  hipStream_t stream2 = nullptr; /* second stream of the pipelined scans */
+  hipEvent_t gev[GD_MAX_GROUPS] = {};
   char *ws = nullptr;
   size_t ws_cap = 0;
   double *gscratch = nullptr;
   size_t gscratch_cap = 0; /* doubles */
   uint64_t *binom = nullptr;
+  /* FET score table, cached across scans for the last (asize, bsize) */
+  int *lut_hdr = nullptr;
+  double *lut = nullptr;
   /* host-API staging buffers (device) */
   char *io = nullptr;
   size_t io_cap = 0;
@@ -85,10 +96,15 @@ static int ctx_init(gd_ctx *c, int device) {
   c->device = device;
   HIP_TRY(hipSetDevice(device));
   HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+  HIP_TRY(hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking));
+  for (auto &e : c->gev) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   HIP_TRY(hipMalloc(&c->binom, sizeof(uint64_t) * GD_BINOM_ENTRIES));
   hipLaunchKernelGGL(k_binom_table, dim3((GD_BINOM_ENTRIES + 255) / 256), dim3(256), 0, c->stream, c->binom);
   HIP_TRY(hipGetLastError());
   for (auto &e : c->ev) HIP_TRY(hipEventCreate(&e));
+  HIP_TRY(hipMalloc(&c->lut_hdr, 4 * sizeof(int)));
+  HIP_TRY(hipMemsetAsync(c->lut_hdr, 0, 4 * sizeof(int), c->stream));
+  HIP_TRY(hipMalloc(&c->lut, sizeof(double) * GD_LUT_CAP));
   HIP_TRY(hipHostMalloc(&c->h_flags, 64));
   HIP_TRY(hipStreamSynchronize(c->stream));
   return GD_OK;
@@ -110,9 +126,14 @@ extern "C" void gd_ctx_destroy(gd_ctx *c) {
   (void)hipFree(c->ws);
   (void)hipFree(c->gscratch);
   (void)hipFree(c->binom);
+  (void)hipFree(c->lut_hdr);
+  (void)hipFree(c->lut);
   (void)hipFree(c->io);
   for (auto &e : c->ev)
     if (e) (void)hipEventDestroy(e);
+  for (auto &e : c->gev)
+    if (e) (void)hipEventDestroy(e);
+  if (c->stream2) (void)hipStreamDestroy(c->stream2);
   if (c->h_flags) (void)hipHostFree(c->h_flags);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
@@ -244,10 +265,16 @@ static int fet_scan_locked(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, cons
   if (pl.wtotal == 0) return GD_OK;
   HIP_TRY(hipSetDevice(ctx->device));
 
+  /* fast-kernel workgroups are aligned to chromosomes: blk_off[c] = first workgroup of c */
+  const int wpb = gd_fet_fast_windows_per_block();
+  std::vector<int32_t> blk_off(nchrom + 1, 0);
+  for (int c = 0; c < nchrom; ++c) blk_off[c + 1] = blk_off[c] + (pl.h[c].wend + wpb - 1) / wpb;
+
   Carve cv{nullptr};
-  auto layout = [&](Carve &k, gd_chrom_dev **d_ch, unsigned **flags, int32_t **lo_a, int32_t **hi_a,
-                    int32_t **lo_b, double **snp, int32_t **list, int32_t **huge) {
+  auto layout = [&](Carve &k, gd_chrom_dev **d_ch, int32_t **d_blk, unsigned **flags, int32_t **lo_a,
+                    int32_t **hi_a, int32_t **lo_b, double **snp, int32_t **list, int32_t **huge) {
     *d_ch = k.take<gd_chrom_dev>(nchrom);
+    *d_blk = k.take<int32_t>(nchrom + 1);
     *flags = k.take<unsigned>(16);
     *lo_a = k.take<int32_t>(pl.wtotal);
     *hi_a = k.take<int32_t>(pl.wtotal);
@@ -258,37 +285,62 @@ static int fet_scan_locked(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, cons
   };
   gd_chrom_dev *d_ch;
   unsigned *flags;
-  int32_t *lo_a, *hi_a, *lo_b, *list, *huge;
+  int32_t *d_blk, *lo_a, *hi_a, *lo_b, *list, *huge;
   double *snp;
-  layout(cv, &d_ch, &flags, &lo_a, &hi_a, &lo_b, &snp, &list, &huge);
+  layout(cv, &d_ch, &d_blk, &flags, &lo_a, &hi_a, &lo_b, &snp, &list, &huge);
   if ((st = grow(&ctx->ws, &ctx->ws_cap, cv.off))) return st;
   Carve real{ctx->ws};
-  layout(real, &d_ch, &flags, &lo_a, &hi_a, &lo_b, &snp, &list, &huge);
+  layout(real, &d_ch, &d_blk, &flags, &lo_a, &hi_a, &lo_b, &snp, &list, &huge);
   unsigned *list_count = flags + 4, *huge_count = flags + 8;
 
   HIP_TRY(hipMemcpyAsync(d_ch, pl.h.data(), sizeof(gd_chrom_dev) * nchrom, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(d_blk, blk_off.data(), sizeof(int32_t) * (nchrom + 1), hipMemcpyHostToDevice, s));
   HIP_TRY(hipMemsetAsync(flags, 0, 16 * sizeof(unsigned), s));
   HIP_TRY(hipEventRecord(ctx->ev[0], s));
   hipLaunchKernelGGL(k_popsize, dim3(nchrom), dim3(64), 0, s, d_ch, apos, bpos, flags);
-  {
-    const int64_t mx = std::max(pl.max_alen, pl.max_blen) + 1;
-    const unsigned gx = (unsigned)std::min<int64_t>((mx + 255) / 256, 2048);
-    hipLaunchKernelGGL(k_bounds, dim3(gx, nchrom, 2), dim3(256), 0, s, d_ch, apos, bpos, wsize, wstep, lo_a,
+  bool force_general = false;
+  if ((st = gd_fet_window_prepare(pl.wtotal, list, list_count, s, &force_general))) return st;
+  /* score table for chromosome 0's population sizes (no-op when cached) */
+  hipLaunchKernelGGL(k_fet_lut_build, dim3(512), dim3(256), 0, s, d_ch, ctx->binom, ctx->lut_hdr, ctx->lut,
+                     (int64_t)GD_LUT_CAP);
+  hipLaunchKernelGGL(k_fet_lut_publish, dim3(1), dim3(1), 0, s, d_ch, ctx->lut_hdr, (int64_t)GD_LUT_CAP);
+
+  /* Pipeline over chromosome groups: the HBM-bound passes (bounds + per-SNP FET)
+   * of group g+1 run on stream s while the VALU-bound bootstrap of group g runs on
+   * the context's second stream. */
+  int G = std::min(nchrom, GD_MAX_GROUPS);
+  if (const char *eg = getenv("GD_GROUPS")) G = std::max(1, std::min(G, atoi(eg))); /* diagnostics */
+  std::vector<int> cuts(G + 1);
+  for (int g = 0; g <= G; ++g) cuts[g] = (int)((int64_t)nchrom * g / G);
+  for (int g = 0; g < G; ++g) {
+    const int c0 = cuts[g], nc = cuts[g + 1] - cuts[g];
+    if (nc <= 0) continue;
+    int64_t amax = 1, mx = 1;
+    for (int c = c0; c < c0 + nc; ++c) {
+      amax = std::max<int64_t>(amax, pl.h[c].alen);
+      mx = std::max<int64_t>(mx, std::max(pl.h[c].alen, pl.h[c].blen) + 1);
+    }
+    const unsigned gxb = (unsigned)std::min<int64_t>((mx + 4095) / 4096, std::max(1, 8192 / nc));
+    hipLaunchKernelGGL(k_bounds, dim3(gxb, nc, 2), dim3(256), 0, s, d_ch + c0, apos, bpos, wsize, wstep, lo_a,
                        hi_a, lo_b, flags);
+    const unsigned gxs = (unsigned)std::min<int64_t>((amax + 255) / 256, std::max(1, 8192 / nc));
+    hipLaunchKernelGGL(k_snp_fet, dim3(gxs, nc), dim3(256), 0, s, d_ch + c0, avals, bvals, ctx->binom,
+                       ctx->lut_hdr, ctx->lut, snp);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(ctx->gev[g], s));
   }
-  HIP_TRY(hipGetLastError());
   HIP_TRY(hipEventRecord(ctx->ev[1], s));
-  {
-    const unsigned gx = (unsigned)std::min<int64_t>((pl.max_alen + 255) / 256, std::max(1, 8192 / nchrom));
-    hipLaunchKernelGGL(k_snp_fet, dim3(std::max(gx, 1u), nchrom), dim3(256), 0, s, d_ch, avals, bvals,
-                       ctx->binom, snp);
+  hipStream_t s2 = ctx->stream2;
+  HIP_TRY(hipStreamWaitEvent(s2, ctx->ev[0], 0));
+  for (int g = 0; g < G && !force_general; ++g) {
+    const int c0 = cuts[g], c1 = cuts[g + 1];
+    HIP_TRY(hipStreamWaitEvent(s2, ctx->gev[g], 0));
+    st = gd_fet_window_fast_launch(d_ch, nchrom, d_blk, blk_off[c0], blk_off[c1] - blk_off[c0], lo_a, hi_a, lo_b,
+                                   snp, perc, scores, stddev, flags, list, list_count, s2);
+    if (st) return fail(st, "fast window kernel launch failed");
   }
-  HIP_TRY(hipGetLastError());
-  HIP_TRY(hipEventRecord(ctx->ev[2], s));
-  st = gd_fet_window_fast_launch(d_ch, nchrom, pl.wtotal, lo_a, hi_a, lo_b, snp, perc, scores, stddev, flags,
-                                 list, list_count, s);
-  if (st) return st;
-  HIP_TRY(hipEventRecord(ctx->ev[3], s));
+  HIP_TRY(hipEventRecord(ctx->ev[2], s2));
+  HIP_TRY(hipStreamWaitEvent(s, ctx->ev[2], 0));
   {
     /* windows the fast path declined: literal one-workgroup-per-window path */
     const unsigned gx = (unsigned)std::min<int64_t>(pl.wtotal, 4096);
@@ -297,7 +349,7 @@ static int fet_scan_locked(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, cons
                        stddev, flags, huge, huge_count, (double *)nullptr, (int64_t)0);
   }
   HIP_TRY(hipGetLastError());
-  HIP_TRY(hipEventRecord(ctx->ev[4], s));
+  HIP_TRY(hipEventRecord(ctx->ev[3], s));
   HIP_TRY(hipMemcpyAsync(ctx->h_flags, flags, 16 * sizeof(unsigned), hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
   const unsigned nhuge = ctx->h_flags[8];
@@ -323,8 +375,12 @@ static int fet_scan_locked(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, cons
     HIP_TRY(hipStreamSynchronize(s));
   }
   float ms;
-  for (int i = 0; i < GD_NSTAGES; ++i)
-    if (hipEventElapsedTime(&ms, ctx->ev[i], ctx->ev[i + 1]) == hipSuccess) g_stage_ms[i] = ms;
+  /* stage times on the scan's streams: memory passes, end of the bootstrap, end of
+   * the general path, all measured from the scan's first kernel */
+  if (hipEventElapsedTime(&ms, ctx->ev[0], ctx->ev[1]) == hipSuccess) g_stage_ms[GD_STAGE_MEM] = ms;
+  if (hipEventElapsedTime(&ms, ctx->ev[0], ctx->ev[2]) == hipSuccess) g_stage_ms[GD_STAGE_WINDOW] = ms;
+  if (hipEventElapsedTime(&ms, ctx->ev[2], ctx->ev[3]) == hipSuccess) g_stage_ms[GD_STAGE_GENERAL] = ms;
+  if (hipEventElapsedTime(&ms, ctx->ev[0], ctx->ev[3]) == hipSuccess) g_stage_ms[GD_STAGE_TOTAL] = ms;
   return flags_to_status(ctx->h_flags[0]);
 }
 

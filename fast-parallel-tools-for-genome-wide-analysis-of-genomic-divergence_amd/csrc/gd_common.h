@@ -171,6 +171,9 @@ GD_HD uint64_t gd_binomial_ref(uint64_t n, uint64_t k) {
   return acc;
 }
 
+/* index of the count pair (maj, min), maj + min <= size, in row-major triangular order */
+GD_HD int gd_pair_index(int maj, int mnr, int size) { return maj * (size + 1) - maj * (maj - 1) / 2 + mnr; }
+
 /* Triangular table of gd_binomial_ref(n, k) for 0 <= k <= n <= GD_BINOM_NMAX. */
 #define GD_BINOM_NMAX 255
 GD_HD int gd_binom_index(int n, int k) { return n * (n + 1) / 2 + k; }

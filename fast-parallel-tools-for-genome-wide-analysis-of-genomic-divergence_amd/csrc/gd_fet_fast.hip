@@ -19,12 +19,12 @@
  * windows with NaN scores, n < 2, n > NFAST, m > 8, misaligned A/B rows, or a
  * replicate whose order statistic falls below the ranked top-KTOP.
  *
- * Layout: 256-thread workgroup = 32 consecutive windows x 8 lanes; lanes of a
- * window split its 100 replicates 13/13/.../9.  Windows are assigned to lane
- * groups in order of n, so the 8 windows of a wave run loops of similar length.
- * The SNP scores the 32 windows touch (a contiguous row span of one chromosome)
- * are staged in LDS once.  Per draw: 6 VALU for the LCG step, 4 for r mod n,
- * MT (4 or 8, chosen per workgroup) for the order statistics, 1/2 for the
+ * Layout: 256-thread workgroup = 32 consecutive windows of one chromosome x 8
+ * lanes; lanes run 13 of the window's 100 replicates (the last 9).  Windows are assigned
+ * to lane groups in order of n, so the windows sharing a wave run loops of similar
+ * length.  The SNP scores the 32 windows touch (a contiguous row span) are staged
+ * in LDS once.  Per draw: 4 VALU for the LCG step (FW_DRAW), 5 for the draw and
+ * r mod n, MT (4 or 8, chosen per workgroup) for the order statistics, 1 for the
  * rejection maximum.
  */
 #include <hip/hip_runtime.h>
@@ -36,11 +36,15 @@
 #include "gd_internal.h"
 
 #define FW_WPB 32    /* windows per workgroup */
-#define FW_TPW 8     /* lanes per window */
-#define FW_RPT 13    /* replicates per lane (8*13 >= 100) */
+#define FW_TPW 8     /* lanes per window (10 and 4 measured 35% / 22% slower) */
+#define FW_RPT 13    /* replicates per lane (8*13 >= 100; the last lane runs 9) */
 #define FW_KTOP 32   /* ranked top scores kept per window */
 #define FW_NFAST 256 /* largest window handled here */
 #define FW_SPAN 2048 /* staged SNP rows per workgroup */
+#define FW_MAXREJ 8  /* rejected draws tracked per window before giving up */
+
+#define FW_BAD_GENERAL 1 /* hand the window to the literal general path */
+#define FW_BAD_REJECT 2  /* a draw was rejected: redo with corrected offsets (B') */
 
 namespace {
 
@@ -72,31 +76,39 @@ __device__ __forceinline__ int fmod_n(uint32_t r, uint32_t magic, uint32_t shift
   return (int)(r - q * n);
 }
 
-/* lane's replicates [r0, r1): stream already positioned at r0*n */
+/* The LCG runs on y = x << 16 (mod 2^64): y' = a*y + (c << 16) keeps the 48-bit
+ * nrand48 state in the top 48 bits, so no masking is needed and the 31-bit draw
+ * x' >> 17 is simply the high word >> 1.  Per step: one v_mad_u64_u32, one
+ * v_mul_lo_u32, one v_lshl_add (a's high part is 5), one v_add3. */
+#define FW_C16 (GD_LCG_C << 16)
+
+/* one draw: advance, extract, reduce mod n, insert into the top-MT list */
+#define FW_DRAW(MT)                                                  \
+  do {                                                               \
+    y = y * GD_LCG_A + FW_C16;                                       \
+    const uint32_t hi_ = (uint32_t)(y >> 32);                        \
+    ymax = max(ymax, hi_);                                           \
+    top_insert<MT>(K, fmod_n(hi_ >> 1, rd.magic, rd.shift, rd.n));   \
+  } while (0)
+
+/* lane's replicates [r0, r1): y already positioned at stream position r0*n.
+ * ymax collects the high words; a draw was rejected iff (ymax >> 1) > limit. */
 template <int MT>
-__device__ __forceinline__ void boot_lane(uint64_t x, int n, const gd_randint &rd, int r0, int r1, int m, int base,
-                                          double delta, const double *top, double *rep, uint32_t &rmax,
+__device__ __forceinline__ void boot_lane(uint64_t y, int n, const gd_randint &rd, int r0, int r1, int m, int base,
+                                          double delta, const double *top, double *rep, uint32_t &ymax,
                                           int &worst) {
   for (int r = r0; r < r1; ++r) {
     int K[MT];
 #pragma unroll
     for (int i = 0; i < MT; ++i) K[i] = -1;
     int j = n;
-    for (; j >= 2; j -= 2) {
-      x = gd_lcg_next(x);
-      const uint32_t ra = gd_lcg_value(x);
-      x = gd_lcg_next(x);
-      const uint32_t rb = gd_lcg_value(x);
-      rmax = max(rmax, max(ra, rb));
-      top_insert<MT>(K, fmod_n(ra, rd.magic, rd.shift, rd.n));
-      top_insert<MT>(K, fmod_n(rb, rd.magic, rd.shift, rd.n));
+    for (; j >= 4; j -= 4) {
+      FW_DRAW(MT);
+      FW_DRAW(MT);
+      FW_DRAW(MT);
+      FW_DRAW(MT);
     }
-    if (j) {
-      x = gd_lcg_next(x);
-      const uint32_t ra = gd_lcg_value(x);
-      rmax = max(rmax, ra);
-      top_insert<MT>(K, fmod_n(ra, rd.magic, rd.shift, rd.n));
-    }
+    for (; j > 0; --j) FW_DRAW(MT);
     int a = K[0], b = K[0];
 #pragma unroll
     for (int i = 0; i < MT; ++i) {
@@ -104,6 +116,34 @@ __device__ __forceinline__ void boot_lane(uint64_t x, int n, const gd_randint &r
       if (i == m - 2) b = K[i];
     }
     worst = min(worst, a); /* a = t_{m-1} <= b = t_{m-2}: the lowest index read */
+    rep[r] = gd_perc_mix(delta, top[max(a - base, 0)], top[max(b - base, 0)]);
+  }
+}
+
+/* Rare second pass for a window whose stream contains rejected draws
+ * (random_int_nrand48 redraws while r > limit, cFisher.c:550-552): every draw
+ * loops until accepted, starting from the lane's corrected stream position. */
+__device__ void boot_lane_rejecting(uint64_t y, int n, const gd_randint &rd, int r0, int r1, int m, int base,
+                                    double delta, const double *top, double *rep, int &worst) {
+  for (int r = r0; r < r1; ++r) {
+    int K[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) K[i] = -1;
+    for (int j = 0; j < n; ++j) {
+      uint32_t hi;
+      do {
+        y = y * GD_LCG_A + FW_C16;
+        hi = (uint32_t)(y >> 32);
+      } while ((hi >> 1) > rd.limit);
+      top_insert<8>(K, fmod_n(hi >> 1, rd.magic, rd.shift, rd.n));
+    }
+    int a = K[0], b = K[0];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      if (i == m - 1) a = K[i];
+      if (i == m - 2) b = K[i];
+    }
+    worst = min(worst, a);
     rep[r] = gd_perc_mix(delta, top[max(a - base, 0)], top[max(b - base, 0)]);
   }
 }
@@ -126,29 +166,44 @@ __device__ double std_reverse_lds(const double *a) {
 }  // namespace
 
 __global__ void __launch_bounds__(FW_WPB *FW_TPW)
-    k_fet_window_fast(const gd_chrom_dev *ch, int nchrom, int64_t wtotal, const int32_t *lo_a,
-                      const int32_t *hi_a, const int32_t *lo_b, const double *snp_score, double perc,
-                      double *scores, double *stddev, const unsigned *flags, int32_t *slow_list,
+    k_fet_window_fast(const gd_chrom_dev *ch, int nchrom, const int32_t *blk_off, int blk_base,
+                      const int32_t *lo_a, const int32_t *hi_a, const int32_t *lo_b, const double *snp_score,
+                      double perc, double *scores, double *stddev, const unsigned *flags, int32_t *slow_list,
                       unsigned *slow_count) {
   __shared__ double sh_span[FW_SPAN];
   __shared__ double sh_top[FW_WPB][FW_KTOP];
   __shared__ double sh_rep[FW_WPB][GD_NREP];
   __shared__ int64_t sh_row[FW_WPB]; /* snp_score index of the window's first row; -1: not fast */
-  __shared__ int sh_n[FW_WPB], sh_c[FW_WPB], sh_bad[FW_WPB], sh_slot[FW_WPB];
+  __shared__ int sh_n[FW_WPB], sh_c[FW_WPB], sh_bad[FW_WPB], sh_slot[FW_WPB], sh_nrej[FW_WPB];
+  __shared__ int sh_rej[FW_WPB][FW_MAXREJ];
   __shared__ int64_t sh_span0;
-  __shared__ int sh_spanlen, sh_mmax;
+  __shared__ int sh_spanlen;
 
   if (*flags & (GD_FLAG_UNSORTED_A | GD_FLAG_UNSORTED_B | GD_FLAG_BAD_SIZE)) return;
   const int tid = threadIdx.x;
-  const int64_t g0 = (int64_t)blockIdx.x * FW_WPB;
+  /* workgroups never straddle chromosomes: blk_off[c] = first workgroup of chromosome c */
+  const int b = blk_base + blockIdx.x;
+  int cb = 0;
+  {
+    int lo = 0, hi = nchrom - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (blk_off[mid] <= b)
+        lo = mid;
+      else
+        hi = mid - 1;
+    }
+    cb = lo;
+  }
+  const int64_t g0 = ch[cb].w_base + (int64_t)(b - blk_off[cb]) * FW_WPB;
+  const int64_t wtotal = ch[cb].w_base + ch[cb].wend; /* end of this chromosome's windows */
 
   /* ---- A1. window extents (one lane per window) ---- */
   if (tid < FW_WPB) {
     const int64_t g = g0 + tid;
     int64_t row = -1;
-    int n = 0, c = 0;
+    int n = 0, c = cb;
     if (g < wtotal) {
-      c = chrom_of_fast(ch, nchrom, g);
       const gd_chrom_dev &d = ch[c];
       const int lo = lo_a[g], hi = hi_a[g], lb = lo_b[g];
       n = (hi - lo) / d.asize;
@@ -162,7 +217,6 @@ __global__ void __launch_bounds__(FW_WPB *FW_TPW)
     sh_c[tid] = c;
     sh_bad[tid] = 0;
   }
-  if (tid == 0) sh_mmax = 0;
   __syncthreads();
   if (tid == 0) {
     /* one chromosome's contiguous row span: that of the first fast window */
@@ -185,12 +239,18 @@ __global__ void __launch_bounds__(FW_WPB *FW_TPW)
     sh_spanlen = (s0 >= 0) ? (int)(s1 - s0) : 0;
   }
   __syncthreads();
-  /* lane groups take windows in order of n (non-fast windows first, they are idle) */
+  /* lane groups take windows in order of (m, n) (non-fast windows first, they are
+   * idle): the windows of a wave then need the same number of order statistics
+   * and run draw loops of similar length */
   if (tid < FW_WPB) {
-    const int key = sh_row[tid] >= 0 ? sh_n[tid] : -1;
+    auto key_of = [&](int j) {
+      const int nj = sh_n[j];
+      return sh_row[j] >= 0 ? ((nj - gd_perc_index(nj, perc)) << 12) + nj : -1;
+    };
+    const int key = key_of(tid);
     int rank = 0;
     for (int j = 0; j < FW_WPB; ++j) {
-      const int kj = sh_row[j] >= 0 ? sh_n[j] : -1;
+      const int kj = key_of(j);
       rank += (kj < key) || (kj == key && j < tid);
     }
     sh_slot[rank] = tid;
@@ -216,42 +276,89 @@ __global__ void __launch_bounds__(FW_WPB *FW_TPW)
       const double v = S[i];
       nan |= (v != v);
       int rank = 0;
+#pragma unroll 4
       for (int j = 0; j < i; ++j) rank += (S[j] <= v);
+#pragma unroll 4
       for (int j = i + 1; j < n; ++j) rank += (S[j] < v);
       if (rank >= base) sh_top[wl][rank - base] = v;
     }
-    if (nan) sh_bad[wl] = 1;
-    if (q == 0) atomicMax(&sh_mmax, m);
+    if (nan) sh_bad[wl] = FW_BAD_GENERAL;
   }
   __syncthreads();
 
   /* ---- B. bootstrap replicates: lane q runs replicates [13q, 13q+13) ---- */
-  const int mmax = sh_mmax;
+  /* order statistics tracked: the largest m among this wave's fast windows */
+  int mmax = (fast && sh_bad[wl] == 0) ? m : 0;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) mmax = max(mmax, __shfl_xor(mmax, o));
+  const int r0 = q * FW_RPT;
+  const int r1 = min(GD_NREP, r0 + FW_RPT);
+  const double delta = gd_perc_delta(n > 0 ? n : 1, perc, idx);
+  const gd_randint rd = gd_randint_make((uint32_t)(n > 0 ? n : 1));
+  uint64_t x0 = 0;
+  if (fast) x0 = gd_window_state(ch[sh_c[wl]].seed, GD_STREAM_FET, g - ch[sh_c[wl]].w_base);
   if (fast && sh_bad[wl] == 0) {
-    const gd_chrom_dev &d = ch[sh_c[wl]];
-    const double delta = gd_perc_delta(n, perc, idx);
-    const gd_randint rd = gd_randint_make((uint32_t)n);
-    const int r0 = q * FW_RPT;
-    const int r1 = min(GD_NREP, r0 + FW_RPT);
-    uint64_t x = gd_window_state(d.seed, GD_STREAM_FET, g - d.w_base);
-    x = gd_affine_apply(gd_lcg_jump((uint64_t)r0 * (uint64_t)n), x);
-    uint32_t rmax = 0;
+    const uint64_t x = gd_affine_apply(gd_lcg_jump((uint64_t)r0 * (uint64_t)n), x0);
+    uint32_t ymax = 0;
     int worst = n;
     if (mmax <= 4)
-      boot_lane<4>(x, n, rd, r0, r1, m, base, delta, sh_top[wl], sh_rep[wl], rmax, worst);
+      boot_lane<4>(x << 16, n, rd, r0, r1, m, base, delta, sh_top[wl], sh_rep[wl], ymax, worst);
+    else if (mmax == 5)
+      boot_lane<5>(x << 16, n, rd, r0, r1, m, base, delta, sh_top[wl], sh_rep[wl], ymax, worst);
     else
-      boot_lane<8>(x, n, rd, r0, r1, m, base, delta, sh_top[wl], sh_rep[wl], rmax, worst);
-    if (rmax > rd.limit || worst < base) atomicOr(&sh_bad[wl], 1);
+      boot_lane<8>(x << 16, n, rd, r0, r1, m, base, delta, sh_top[wl], sh_rep[wl], ymax, worst);
+    if (worst < base) atomicOr(&sh_bad[wl], FW_BAD_GENERAL);
+    if ((ymax >> 1) > rd.limit) atomicOr(&sh_bad[wl], FW_BAD_REJECT);
+  }
+  __syncthreads();
+
+  /* ---- B'. windows whose stream rejected a draw (p ~ n*5000/2^31 per window):
+   * lane q locates the rejected positions of its pass-1 range [13qn, 13qn + len),
+   * the lanes then restart at the corrected positions P_q = 13qn + #(rejections
+   * before P_q) and redraw with the rejection loop.  Whole-workgroup branch,
+   * taken by ~1 in 300 workgroups. */
+  if (fast && sh_bad[wl] == FW_BAD_REJECT && q == 0) sh_nrej[wl] = 0;
+  __syncthreads();
+  if (fast && sh_bad[wl] == FW_BAD_REJECT) {
+    const int64_t p0 = (int64_t)r0 * n, len = (int64_t)(r1 - r0) * n;
+    uint64_t y = gd_affine_apply(gd_lcg_jump((uint64_t)p0), x0) << 16;
+    for (int64_t t = 0; t < len; ++t) {
+      y = y * GD_LCG_A + FW_C16;
+      if (((uint32_t)(y >> 32) >> 1) > rd.limit) {
+        const int k = atomicAdd(&sh_nrej[wl], 1);
+        if (k < FW_MAXREJ) sh_rej[wl][k] = (int)(p0 + t);
+      }
+    }
+  }
+  __syncthreads();
+  if (fast && sh_bad[wl] == FW_BAD_REJECT) {
+    const int nrej = sh_nrej[wl];
+    if (nrej > FW_MAXREJ) {
+      if (q == 0) sh_bad[wl] |= FW_BAD_GENERAL;
+    } else {
+      /* fixed point: P = 13qn + #(rejected positions < P); all such positions lie in [0, 100n) */
+      int64_t c = 0;
+      for (;;) {
+        const int64_t P = (int64_t)r0 * n + c;
+        int64_t cnt = 0;
+        for (int k = 0; k < nrej; ++k) cnt += (sh_rej[wl][k] < P);
+        if (cnt == c) break;
+        c = cnt;
+      }
+      const uint64_t y = gd_affine_apply(gd_lcg_jump((uint64_t)r0 * n + c), x0) << 16;
+      int worst = n;
+      boot_lane_rejecting(y, n, rd, r0, r1, m, base, delta, sh_top[wl], sh_rep[wl], worst);
+      if (worst < base) atomicOr(&sh_bad[wl], FW_BAD_GENERAL);
+    }
   }
   __syncthreads();
 
   /* ---- C. window score + population std of the 100 replicates ---- */
   if (fast && q == 0) {
     const gd_chrom_dev &d = ch[sh_c[wl]];
-    if (sh_bad[wl]) {
+    if (sh_bad[wl] & FW_BAD_GENERAL) {
       slow_list[atomicAdd(slow_count, 1u)] = (int32_t)g;
     } else {
-      const double delta = gd_perc_delta(n, perc, idx);
       const int idx1 = (idx + 1 < n) ? idx + 1 : idx;
       const double ws = gd_perc_mix(delta, sh_top[wl][idx - base], sh_top[wl][idx1 - base]);
       const int64_t w = g - d.w_base;
@@ -270,19 +377,29 @@ __global__ void k_all_windows(int32_t *list, unsigned *count, int64_t wtotal) {
   if (i == 0) *count = (unsigned)wtotal;
 }
 
-int gd_fet_window_fast_launch(const gd_chrom_dev *ch, int nchrom, int64_t wtotal, const int32_t *lo_a,
-                              const int32_t *hi_a, const int32_t *lo_b, const double *snp_score, double perc,
-                              double *scores, double *stddev, unsigned *flags, int32_t *slow_list,
-                              unsigned *slow_count, hipStream_t s) {
+int gd_fet_fast_windows_per_block() { return FW_WPB; }
+
+/* Resets the slow-path list; with GD_FORCE_GENERAL=1 fills it with every window and
+ * tells the caller to skip the fast kernels. */
+int gd_fet_window_prepare(int64_t wtotal, int32_t *slow_list, unsigned *slow_count, hipStream_t s,
+                          bool *force_general) {
   const char *force = getenv("GD_FORCE_GENERAL");
-  if (force && force[0] == '1') {
+  *force_general = force && force[0] == '1';
+  if (*force_general)
     hipLaunchKernelGGL(k_all_windows, dim3((unsigned)((wtotal + 255) / 256)), dim3(256), 0, s, slow_list,
                        slow_count, wtotal);
-    return hipGetLastError() == hipSuccess ? GD_OK : GD_ERR_HIP;
-  }
-  hipLaunchKernelGGL(k_zero_count, dim3(1), dim3(1), 0, s, slow_count);
-  const unsigned blocks = (unsigned)((wtotal + FW_WPB - 1) / FW_WPB);
-  hipLaunchKernelGGL(k_fet_window_fast, dim3(blocks), dim3(FW_WPB * FW_TPW), 0, s, ch, nchrom, wtotal, lo_a, hi_a,
-                     lo_b, snp_score, perc, scores, stddev, flags, slow_list, slow_count);
+  else
+    hipLaunchKernelGGL(k_zero_count, dim3(1), dim3(1), 0, s, slow_count);
+  return hipGetLastError() == hipSuccess ? GD_OK : GD_ERR_HIP;
+}
+
+/* workgroups [blk_begin, blk_begin + blk_count) of the chromosome-aligned grid */
+int gd_fet_window_fast_launch(const gd_chrom_dev *ch, int nchrom, const int32_t *blk_off, int blk_begin,
+                              int blk_count, const int32_t *lo_a, const int32_t *hi_a, const int32_t *lo_b,
+                              const double *snp_score, double perc, double *scores, double *stddev,
+                              unsigned *flags, int32_t *slow_list, unsigned *slow_count, hipStream_t s) {
+  if (blk_count <= 0) return GD_OK;
+  hipLaunchKernelGGL(k_fet_window_fast, dim3((unsigned)blk_count), dim3(FW_WPB * FW_TPW), 0, s, ch, nchrom, blk_off,
+                     blk_begin, lo_a, hi_a, lo_b, snp_score, perc, scores, stddev, flags, slow_list, slow_count);
   return hipGetLastError() == hipSuccess ? GD_OK : GD_ERR_HIP;
 }

@@ -170,25 +170,57 @@ __global__ void __launch_bounds__(256) k_bounds(const gd_chrom_dev *ch, const in
   int32_t *lo = (pop ? lo_b : lo_a) + d.w_base;
   int32_t *hi = hi_a + d.w_base;
   const double inv = 1.0 / (double)wstep;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x * 4;
+  const bool aligned16 = ((pop ? d.b_off : d.a_off) & 3) == 0; /* int4 loads stay 16-byte aligned */
+  /* each lane scans 16 consecutive elements (chromosome-relative i in [i0, i0+16)),
+   * packs the offsets of its boundaries (i == 0, i == len, or pos[i] != pos[i-1])
+   * as 4-bit nibbles, then handles just those: a wave runs the window-range code
+   * max-boundaries-per-lane times (~1-2 at 20 individuals), not once per element */
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x * 16;
   bool unsorted = false;
-  for (int64_t i0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4; i0 <= len; i0 += stride) {
-    int32_t v[5];
+  for (int64_t i0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 16; i0 <= len; i0 += stride) {
+    int32_t prev = (i0 > 0) ? pos[i0 - 1] : 0;
+    uint64_t nib = 0;
+    int nb = 0;
+    if (i0 + 16 <= len) {
+      int32_t v16[16];
+      if (aligned16) {
 #pragma unroll
-    for (int k = 0; k < 5; ++k) {
-      const int64_t i = i0 - 1 + k;
-      v[k] = (i >= 0 && i < len) ? pos[i] : 0;
-    }
+        for (int k = 0; k < 4; ++k) {
+          const int4 t = *reinterpret_cast<const int4 *>(pos + i0 + 4 * k);
+          v16[4 * k] = t.x;
+          v16[4 * k + 1] = t.y;
+          v16[4 * k + 2] = t.z;
+          v16[4 * k + 3] = t.w;
+        }
+      } else {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int64_t i = i0 + k;
-      if (i > len) break;
-      const bool first = (i == 0), last = (i == len);
-      const int64_t p = v[k + 1], pp = v[k];
-      if (!first && !last) {
-        if (p == pp) continue;
-        unsorted |= (p < pp);
+        for (int k = 0; k < 16; ++k) v16[k] = pos[i0 + k];
       }
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const int32_t v = v16[k];
+        const bool bnd = (v != prev) || (i0 + k == 0);
+        unsorted |= (i0 + k > 0) && (v < prev);
+        nib |= bnd ? ((uint64_t)k << (4 * nb)) : 0;
+        nb += bnd;
+        prev = v;
+      }
+    } else {
+      for (int k = 0; k < 16 && i0 + k <= len; ++k) {
+        const int64_t i = i0 + k;
+        const int32_t v = (i < len) ? pos[i] : 0;
+        const bool bnd = (i == 0) || (i == len) || (v != prev);
+        if (i > 0 && i < len) unsorted |= (v < prev);
+        nib |= bnd ? ((uint64_t)k << (4 * nb)) : 0;
+        nb += bnd;
+        prev = v;
+      }
+    }
+    for (int t = 0; t < nb; ++t) {
+      const int64_t i = i0 + (int)((nib >> (4 * t)) & 15);
+      const bool first = (i == 0), last = (i == len);
+      const int64_t p = last ? 0 : pos[i];
+      const int64_t pp = first ? 0 : pos[i - 1];
       int64_t f = first ? 0 : fdiv_fast(pp, wstep, inv) + 1;
       int64_t l = last ? wend - 1 : fdiv_fast(p, wstep, inv);
       if (f < 0) f = 0;
@@ -239,11 +271,14 @@ __device__ __forceinline__ int count_range(const uint64_t (*m)[2], int s, int e)
 }  // namespace
 
 __global__ void __launch_bounds__(256) k_snp_fet(const gd_chrom_dev *ch, const double *avals, const double *bvals,
-                                                 const uint64_t *binom, double *snp_score) {
+                                                 const uint64_t *binom, const int *lut_hdr, const double *lut,
+                                                 double *snp_score) {
   __shared__ uint64_t sh_m[2][2][SF_MAXCH][2]; /* [pop][maj/min][chunk][even/odd] */
   const gd_chrom_dev &d = ch[blockIdx.y];
   if (d.wend <= 0) return;
   const int nrows = d.nrows, asize = d.asize, bsize = d.bsize;
+  const bool use_lut = lut_hdr[2] == 1 && lut_hdr[0] == asize && lut_hdr[1] == bsize;
+  const int lut_nb = (bsize + 1) * (bsize + 2) / 2;
   const int big = max(asize, bsize);
   const int R = min(256, ((SF_MAXCH - 2) * 128) / max(big, 1));
   if (R <= 0 || nrows <= 0) return;
@@ -289,10 +324,51 @@ __global__ void __launch_bounds__(256) k_snp_fet(const gd_chrom_dev *ch, const d
       const int f1 = count_range(sh_m[0][1], sa, sa + asize);
       const int f2 = count_range(sh_m[1][0], sb, sb + bsize);
       const int f3 = count_range(sh_m[1][1], sb, sb + bsize);
-      snp_score[d.a_off + s0 + r] = gd_fet_score_from_p(fet_p_two_tailed(f0, f1, f2, f3, binom));
+      snp_score[d.a_off + s0 + r] =
+          use_lut ? lut[(int64_t)gd_pair_index(f0, f1, asize) * lut_nb + gd_pair_index(f2, f3, bsize)]
+                  : gd_fet_score_from_p(fet_p_two_tailed(f0, f1, f2, f3, binom));
     }
     __syncthreads();
   }
+}
+
+/* ------------------------------------------------------------------------ */
+/* Score table: -log10 p of every 2x2 table (majA, minA, majB, minB) with      */
+/* majA + minA <= asize and majB + minB <= bsize, computed by the same device */
+/* code as above (so a lookup is bit-identical to a direct evaluation).  Built */
+/* once per (asize, bsize) and kept in the context; k_snp_fet then only counts */
+/* and gathers.  20+20 individuals: 231 x 231 = 53,361 tables (427 KB, L2).    */
+/* hdr = {asize, bsize, valid}.                                                */
+/* ------------------------------------------------------------------------ */
+__global__ void __launch_bounds__(256) k_fet_lut_build(const gd_chrom_dev *ch, const uint64_t *binom,
+                                                       const int *hdr, double *lut, int64_t cap) {
+  const int asize = ch[0].asize, bsize = ch[0].bsize;
+  if (asize <= 0 || bsize <= 0) return;
+  if (hdr[2] == 1 && hdr[0] == asize && hdr[1] == bsize) return; /* cached */
+  const int64_t na = (int64_t)(asize + 1) * (asize + 2) / 2, nb = (int64_t)(bsize + 1) * (bsize + 2) / 2;
+  if (na * nb > cap) return;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < na * nb; e += (int64_t)gridDim.x * blockDim.x) {
+    int ia = (int)(e / nb), ib = (int)(e - (int64_t)ia * nb);
+    int a = 0, c = 0;
+    while (ia >= asize + 1 - a) {
+      ia -= asize + 1 - a;
+      ++a;
+    }
+    while (ib >= bsize + 1 - c) {
+      ib -= bsize + 1 - c;
+      ++c;
+    }
+    lut[e] = gd_fet_score_from_p(fet_p_two_tailed(a, ia, c, ib, binom));
+  }
+}
+
+__global__ void k_fet_lut_publish(const gd_chrom_dev *ch, int *hdr, int64_t cap) {
+  const int asize = ch[0].asize, bsize = ch[0].bsize;
+  const int64_t na = (int64_t)(asize + 1) * (asize + 2) / 2, nb = (int64_t)(bsize + 1) * (bsize + 2) / 2;
+  const bool ok = asize > 0 && bsize > 0 && na * nb <= cap;
+  hdr[0] = asize;
+  hdr[1] = bsize;
+  hdr[2] = ok ? 1 : 0;
 }
 
 /* ------------------------------------------------------------------------ */

@@ -11,7 +11,7 @@ from pathlib import Path
 
 PKG_DIR = Path(__file__).resolve().parent.parent
 LIB_DIR = PKG_DIR / "lib"
-LIB_PATH = LIB_DIR / "libgdscan.so"
+LIB_PATH = Path(os.environ.get("GDSCAN_LIB", LIB_DIR / "libgdscan.so"))  # override: A/B builds
 
 GD_OK = 0
 GD_ERR_ARG = -1

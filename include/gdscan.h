@@ -102,12 +102,16 @@ uint64_t gd_get_seed(void);
 const char *gd_last_error(void);     /* thread-local message for the last failing call */
 int gd_device_count(void);
 
-/* kernel-level timing of the last device scan on this thread (ms, HIP events
- * on the scan's stream), indexed by GD_STAGE_*; returns the number of stages */
-#define GD_STAGE_BOUNDS 0
-#define GD_STAGE_SNP 1
-#define GD_STAGE_WINDOW 2
-#define GD_STAGE_GENERAL 3
+/* timing of the last device scan on this thread (ms, HIP events on the scan's
+ * streams), indexed by GD_STAGE_*; returns the number of stages.
+ *   MEM     first kernel -> end of the HBM-bound passes (window bounds, per-SNP test)
+ *   WINDOW  first kernel -> end of the fast window kernels (overlapped with MEM)
+ *   GENERAL duration of the literal per-window path for declined windows
+ *   TOTAL   first kernel -> last kernel of the scan */
+#define GD_STAGE_MEM 0
+#define GD_STAGE_WINDOW 1
+#define GD_STAGE_GENERAL 2
+#define GD_STAGE_TOTAL 3
 #define GD_NSTAGES 4
 int gd_last_stage_ms(float *ms, int n);
 

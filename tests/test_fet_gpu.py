@@ -203,3 +203,41 @@ def test_fast_path_equals_literal_path_full_chromosome(monkeypatch):
     monkeypatch.delenv("GD_FORCE_GENERAL")
     assert (s_fast != 0).sum() > 49_000
     assert np.array_equal(s_fast, s_lit) and np.array_equal(d_fast, d_lit)
+
+
+def _windows_with_rejections(regend, wsize, wstep, ap, asize, seed, nrep=100):
+    """Host replica of the per-window nrand48 stream: which windows reject a draw."""
+    from gdscan.synth import _mix64
+    nwin = regend // wstep
+    starts = np.arange(nwin) * wstep
+    lo = np.searchsorted(ap, starts, side="left")
+    hi = np.searchsorted(ap, starts + wsize, side="right")
+    n = (hi - lo) // asize
+    w = np.arange(nwin, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        x = _mix64(np.uint64(seed) ^ _mix64(np.uint64(0) + np.uint64(0x9E3779B97F4A7C15) * (w + np.uint64(1))))
+    x &= np.uint64(0xFFFFFFFFFFFF)
+    nn = np.maximum(n, 1).astype(np.int64)
+    limit = 0x7FFFFFFF - (0x80000000 % nn)
+    hit = np.zeros(nwin, bool)
+    for t in range(int(nrep * nn.max())):
+        with np.errstate(over="ignore"):
+            x = (x * np.uint64(0x5DEECE66D) + np.uint64(0xB)) & np.uint64(0xFFFFFFFFFFFF)
+        r = (x >> np.uint64(17)).astype(np.int64)
+        hit |= (r > limit) & (t < nrep * nn)
+    return hit & (n > 0)
+
+
+def test_rejected_draws_are_redrawn(oracle):
+    """Dense windows (n ~ 250, perc 0.99 keeps them on the fast path) make the
+    modulo-bias rejection of random_int_nrand48 (cFisher.c:550-552) happen; the
+    fast path must redraw exactly like the reference."""
+    from gdscan import fet
+    av, bv, ap, bp, regend = _synth(12, 60000, 5, 5)
+    wsize, wstep, perc, seed = 12500, 500, 0.99, 4242
+    hit = _windows_with_rejections(regend, wsize, wstep, ap, 5, seed)
+    assert hit.sum() >= 1
+    s_ref, d_ref = oracle_fet_scan(oracle, av, bv, ap, bp, regend, wsize, wstep, perc, seed)
+    s, d = fet.scan(av, bv, ap, bp, regend, wsize, wstep, perc, seed=seed)
+    assert close(s, s_ref) and close(d, d_ref)
+    assert close(d[hit], d_ref[hit])
