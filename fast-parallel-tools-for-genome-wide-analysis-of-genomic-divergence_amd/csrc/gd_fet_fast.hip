@@ -38,7 +38,7 @@
 #define FW_WPB 32    /* windows per workgroup */
 #define FW_TPW 8     /* lanes per window (10 and 4 measured 35% / 22% slower) */
 #define FW_RPT 13    /* replicates per lane (8*13 >= 100; the last lane runs 9) */
-#define FW_KTOP 32   /* ranked top scores kept per window */
+#define FW_KTOP 24   /* ranked top scores kept per window (P(needing more) < 1e-9 per replicate) */
 #define FW_NFAST 256 /* largest window handled here */
 #define FW_SPAN 2048 /* staged SNP rows per workgroup */
 #define FW_MAXREJ 8  /* rejected draws tracked per window before giving up */
@@ -82,13 +82,21 @@ __device__ __forceinline__ int fmod_n(uint32_t r, uint32_t magic, uint32_t shift
  * v_mul_lo_u32, one v_lshl_add (a's high part is 5), one v_add3. */
 #define FW_C16 (GD_LCG_C << 16)
 
+/* one LCG step on the 32-bit halves of y: lo*a_lo + c16 as one v_mad_u64_u32,
+ * the high word gets hi*a_lo (v_mul_lo_u32) and lo*5 (a's high part; v_lshl_add) */
+#define FW_STEP()                                                              \
+  do {                                                                         \
+    const uint64_t t_ = (uint64_t)ylo * 0xDEECE66Du + FW_C16;                  \
+    yhi = (uint32_t)(t_ >> 32) + yhi * 0xDEECE66Du + ylo * 5u;                 \
+    ylo = (uint32_t)t_;                                                        \
+  } while (0)
+
 /* one draw: advance, extract, reduce mod n, insert into the top-MT list */
 #define FW_DRAW(MT)                                                  \
   do {                                                               \
-    y = y * GD_LCG_A + FW_C16;                                       \
-    const uint32_t hi_ = (uint32_t)(y >> 32);                        \
-    ymax = max(ymax, hi_);                                           \
-    top_insert<MT>(K, fmod_n(hi_ >> 1, rd.magic, rd.shift, rd.n));   \
+    FW_STEP();                                                       \
+    ymax = max(ymax, yhi);                                           \
+    top_insert<MT>(K, fmod_n(yhi >> 1, rd.magic, rd.shift, rd.n));   \
   } while (0)
 
 /* lane's replicates [r0, r1): y already positioned at stream position r0*n.
@@ -97,12 +105,17 @@ template <int MT>
 __device__ __forceinline__ void boot_lane(uint64_t y, int n, const gd_randint &rd, int r0, int r1, int m, int base,
                                           double delta, const double *top, double *rep, uint32_t &ymax,
                                           int &worst) {
+  uint32_t ylo = (uint32_t)y, yhi = (uint32_t)(y >> 32);
   for (int r = r0; r < r1; ++r) {
     int K[MT];
 #pragma unroll
     for (int i = 0; i < MT; ++i) K[i] = -1;
     int j = n;
-    for (; j >= 4; j -= 4) {
+    for (; j >= 8; j -= 8) {
+      FW_DRAW(MT);
+      FW_DRAW(MT);
+      FW_DRAW(MT);
+      FW_DRAW(MT);
       FW_DRAW(MT);
       FW_DRAW(MT);
       FW_DRAW(MT);
@@ -165,6 +178,21 @@ __device__ double std_reverse_lds(const double *a) {
 
 }  // namespace
 
+/* 8-lane DPP max-reduction partners within a lane group: xor 1, xor 2, mirror in 8 */
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const uint64_t u = gd_f64_bits(v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)u, CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(u >> 32), CTRL, 0xF, 0xF, false);
+  return gd_f64_from(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+__device__ __forceinline__ double group8_max(double v) {
+  v = fmax(v, dpp_f64<0xB1>(v));  /* quad_perm [1,0,3,2] */
+  v = fmax(v, dpp_f64<0x4E>(v));  /* quad_perm [2,3,0,1] */
+  v = fmax(v, dpp_f64<0x141>(v)); /* row_half_mirror: lane i <-> 7-i */
+  return v;
+}
+
 __global__ void __launch_bounds__(FW_WPB *FW_TPW)
     k_fet_window_fast(const gd_chrom_dev *ch, int nchrom, const int32_t *blk_off, int blk_base,
                       const int32_t *lo_a, const int32_t *hi_a, const int32_t *lo_b, const double *snp_score,
@@ -172,12 +200,12 @@ __global__ void __launch_bounds__(FW_WPB *FW_TPW)
                       unsigned *slow_count) {
   __shared__ double sh_span[FW_SPAN];
   __shared__ double sh_top[FW_WPB][FW_KTOP];
+  /* the replicate table; before phase B it holds the lanes' locally sorted scores */
   __shared__ double sh_rep[FW_WPB][GD_NREP];
   __shared__ int64_t sh_row[FW_WPB]; /* snp_score index of the window's first row; -1: not fast */
-  __shared__ int sh_n[FW_WPB], sh_c[FW_WPB], sh_bad[FW_WPB], sh_slot[FW_WPB], sh_nrej[FW_WPB];
+  __shared__ int sh_n[FW_WPB], sh_key[FW_WPB], sh_bad[FW_WPB], sh_slot[FW_WPB], sh_nrej[FW_WPB];
   __shared__ int sh_rej[FW_WPB][FW_MAXREJ];
-  __shared__ int64_t sh_span0;
-  __shared__ int sh_spanlen;
+  __shared__ unsigned long long sh_lo, sh_hi;
 
   if (*flags & (GD_FLAG_UNSORTED_A | GD_FLAG_UNSORTED_B | GD_FLAG_BAD_SIZE)) return;
   const int tid = threadIdx.x;
@@ -195,16 +223,21 @@ __global__ void __launch_bounds__(FW_WPB *FW_TPW)
     }
     cb = lo;
   }
-  const int64_t g0 = ch[cb].w_base + (int64_t)(b - blk_off[cb]) * FW_WPB;
-  const int64_t wtotal = ch[cb].w_base + ch[cb].wend; /* end of this chromosome's windows */
+  const gd_chrom_dev &d = ch[cb];
+  const int64_t g0 = d.w_base + (int64_t)(b - blk_off[cb]) * FW_WPB;
+  const int64_t wtotal = d.w_base + d.wend; /* end of this chromosome's windows */
 
-  /* ---- A1. window extents (one lane per window) ---- */
+  /* ---- A1. window extents (one lane per window), the staged row span, lane-group order ---- */
+  if (tid == 0) {
+    sh_lo = ~0ull;
+    sh_hi = 0;
+  }
+  __syncthreads();
   if (tid < FW_WPB) {
     const int64_t g = g0 + tid;
     int64_t row = -1;
-    int n = 0, c = cb;
+    int n = 0;
     if (g < wtotal) {
-      const gd_chrom_dev &d = ch[c];
       const int lo = lo_a[g], hi = hi_a[g], lb = lo_b[g];
       n = (hi - lo) / d.asize;
       const bool aligned = n > 0 && (lo % d.asize == 0) && (lb % d.bsize == 0) && (lo / d.asize == lb / d.bsize) &&
@@ -212,75 +245,103 @@ __global__ void __launch_bounds__(FW_WPB *FW_TPW)
       const int m = n - gd_perc_index(n > 0 ? n : 1, perc);
       if (aligned && n >= 2 && n <= FW_NFAST && m <= 8) row = d.a_off + lo / d.asize;
     }
+    if (row >= 0) atomicMin(&sh_lo, (unsigned long long)row);
     sh_row[tid] = row;
     sh_n[tid] = n;
-    sh_c[tid] = c;
     sh_bad[tid] = 0;
   }
   __syncthreads();
-  if (tid == 0) {
-    /* one chromosome's contiguous row span: that of the first fast window */
-    int64_t s0 = -1, s1 = -1;
-    int cref = -1;
-    for (int i = 0; i < FW_WPB; ++i) {
-      if (sh_row[i] < 0) continue;
-      if (cref < 0) cref = sh_c[i];
-      const int64_t r0 = sh_row[i], r1 = sh_row[i] + sh_n[i];
-      const int64_t n0 = (s0 < 0 || r0 < s0) ? r0 : s0;
-      const int64_t n1 = (r1 > s1) ? r1 : s1;
-      if (sh_c[i] != cref || n1 - n0 > FW_SPAN) {
-        sh_row[i] = -1; /* left to the general path */
-        continue;
-      }
-      s0 = n0;
-      s1 = n1;
-    }
-    sh_span0 = s0;
-    sh_spanlen = (s0 >= 0) ? (int)(s1 - s0) : 0;
+  if (tid < FW_WPB) {
+    /* rows grow with the window index: windows past FW_SPAN staged rows go to the general path */
+    const int64_t row = sh_row[tid];
+    const int n = sh_n[tid];
+    bool fast = row >= 0 && row + n - (int64_t)sh_lo <= FW_SPAN;
+    if (fast) atomicMax(&sh_hi, (unsigned long long)(row + n));
+    if (!fast) sh_row[tid] = -1;
+    sh_key[tid] = fast ? ((n - gd_perc_index(n, perc)) << 12) + n : -1;
+    if (!fast && n > 0 && g0 + tid < wtotal) slow_list[atomicAdd(slow_count, 1u)] = (int32_t)(g0 + tid);
   }
   __syncthreads();
-  /* lane groups take windows in order of (m, n) (non-fast windows first, they are
-   * idle): the windows of a wave then need the same number of order statistics
-   * and run draw loops of similar length */
+  /* lane groups take windows in order of (m, n), non-fast (idle) windows first: the
+   * windows sharing a wave need the same number of order statistics and run draw
+   * loops of similar length */
   if (tid < FW_WPB) {
-    auto key_of = [&](int j) {
-      const int nj = sh_n[j];
-      return sh_row[j] >= 0 ? ((nj - gd_perc_index(nj, perc)) << 12) + nj : -1;
-    };
-    const int key = key_of(tid);
+    const int key = sh_key[tid];
     int rank = 0;
     for (int j = 0; j < FW_WPB; ++j) {
-      const int kj = key_of(j);
+      const int kj = sh_key[j];
       rank += (kj < key) || (kj == key && j < tid);
     }
     sh_slot[rank] = tid;
-    if (sh_row[tid] < 0 && sh_n[tid] > 0 && g0 + tid < wtotal) slow_list[atomicAdd(slow_count, 1u)] = (int32_t)(g0 + tid);
   }
-  const int64_t span0 = sh_span0;
-  for (int i = tid; i < sh_spanlen; i += FW_WPB * FW_TPW) sh_span[i] = snp_score[span0 + i];
+  const int64_t span0 = (int64_t)sh_lo;
+  const int spanlen = sh_hi > sh_lo ? (int)(sh_hi - sh_lo) : 0;
+  for (int i = tid; i < spanlen; i += FW_WPB * FW_TPW) sh_span[i] = snp_score[span0 + i];
   __syncthreads();
 
   const int wl = sh_slot[tid / FW_TPW], q = tid % FW_TPW;
   const int64_t g = g0 + wl;
   const bool fast = sh_row[wl] >= 0;
   const int n = sh_n[wl];
-  const int base = n > FW_KTOP ? n - FW_KTOP : 0;
+  const int ktop = n < FW_KTOP ? n : FW_KTOP;
+  const int base = n - ktop;
   const int idx = gd_perc_index(n > 0 ? n : 1, perc);
   const int m = n - idx;
 
-  /* ---- A2. rank the window's scores (ascending, ties by position) into the top-KTOP table ---- */
+  /* ---- A2. the window's top-KTOP scores in ascending order (sh_top[wl][rank - base]) ---- */
   if (fast) {
     const double *S = sh_span + (sh_row[wl] - span0);
     int nan = 0;
-    for (int i = q; i < n; i += FW_TPW) {
-      const double v = S[i];
-      nan |= (v != v);
-      int rank = 0;
-#pragma unroll 4
-      for (int j = 0; j < i; ++j) rank += (S[j] <= v);
-#pragma unroll 4
-      for (int j = i + 1; j < n; ++j) rank += (S[j] < v);
-      if (rank >= base) sh_top[wl][rank - base] = v;
+    if (n <= FW_TPW * 8) {
+      /* each lane sorts its <= 8 scores (S[q], S[q+8], ...) descending in registers,
+       * stages them in LDS, and the 8 lanes merge: KTOP rounds of an 8-way max */
+      double v[8];
+      int cnt = 0;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int i = q + FW_TPW * u;
+        v[u] = (i < n) ? S[i] : -__builtin_inf();
+        cnt += (i < n);
+        nan |= (i < n) && (v[u] != v[u]);
+      }
+      /* Batcher odd-even merge sort network for 8 keys, descending */
+#define FW_CX(a, b)                         \
+  do {                                      \
+    const double hi_ = fmax(v[a], v[b]);    \
+    v[b] = fmin(v[a], v[b]);                \
+    v[a] = hi_;                             \
+  } while (0)
+      FW_CX(0, 1); FW_CX(2, 3); FW_CX(4, 5); FW_CX(6, 7);
+      FW_CX(0, 2); FW_CX(1, 3); FW_CX(4, 6); FW_CX(5, 7);
+      FW_CX(1, 2); FW_CX(5, 6);
+      FW_CX(0, 4); FW_CX(1, 5); FW_CX(2, 6); FW_CX(3, 7);
+      FW_CX(2, 4); FW_CX(3, 5);
+      FW_CX(1, 2); FW_CX(3, 4); FW_CX(5, 6);
+#undef FW_CX
+      double *mine = &sh_rep[wl][q * 8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) mine[u] = v[u];
+      int h = 0;
+      const int gbase = (threadIdx.x & 63) & ~7; /* first lane of this group in the wave */
+      for (int t = 0; t < ktop; ++t) {
+        const double c = (h < cnt) ? mine[h] : -__builtin_inf();
+        const double cmax = group8_max(c);
+        /* the lowest lane holding the maximum pops it */
+        const uint64_t hit = __ballot(c == cmax);
+        const unsigned grp = (unsigned)(hit >> gbase) & 0xFFu;
+        if (q == __builtin_ctz(grp)) ++h;
+        if (q == 0) sh_top[wl][ktop - 1 - t] = cmax;
+      }
+    } else {
+      /* 64 < n <= NFAST: rank by counting (ties by position) */
+      for (int i = q; i < n; i += FW_TPW) {
+        const double val = S[i];
+        nan |= (val != val);
+        int rank = 0;
+        for (int j = 0; j < i; ++j) rank += (S[j] <= val);
+        for (int j = i + 1; j < n; ++j) rank += (S[j] < val);
+        if (rank >= base) sh_top[wl][rank - base] = val;
+      }
     }
     if (nan) sh_bad[wl] = FW_BAD_GENERAL;
   }
@@ -296,7 +357,7 @@ __global__ void __launch_bounds__(FW_WPB *FW_TPW)
   const double delta = gd_perc_delta(n > 0 ? n : 1, perc, idx);
   const gd_randint rd = gd_randint_make((uint32_t)(n > 0 ? n : 1));
   uint64_t x0 = 0;
-  if (fast) x0 = gd_window_state(ch[sh_c[wl]].seed, GD_STREAM_FET, g - ch[sh_c[wl]].w_base);
+  if (fast) x0 = gd_window_state(d.seed, GD_STREAM_FET, g - d.w_base);
   if (fast && sh_bad[wl] == 0) {
     const uint64_t x = gd_affine_apply(gd_lcg_jump((uint64_t)r0 * (uint64_t)n), x0);
     uint32_t ymax = 0;
@@ -315,8 +376,7 @@ __global__ void __launch_bounds__(FW_WPB *FW_TPW)
   /* ---- B'. windows whose stream rejected a draw (p ~ n*5000/2^31 per window):
    * lane q locates the rejected positions of its pass-1 range [13qn, 13qn + len),
    * the lanes then restart at the corrected positions P_q = 13qn + #(rejections
-   * before P_q) and redraw with the rejection loop.  Whole-workgroup branch,
-   * taken by ~1 in 300 workgroups. */
+   * before P_q) and redraw with the rejection loop.  Taken by ~1 in 300 workgroups. */
   if (fast && sh_bad[wl] == FW_BAD_REJECT && q == 0) sh_nrej[wl] = 0;
   __syncthreads();
   if (fast && sh_bad[wl] == FW_BAD_REJECT) {
@@ -353,17 +413,22 @@ __global__ void __launch_bounds__(FW_WPB *FW_TPW)
   }
   __syncthreads();
 
-  /* ---- C. window score + population std of the 100 replicates ---- */
-  if (fast && q == 0) {
-    const gd_chrom_dev &d = ch[sh_c[wl]];
-    if (sh_bad[wl] & FW_BAD_GENERAL) {
-      slow_list[atomicAdd(slow_count, 1u)] = (int32_t)g;
+  /* ---- C. window score + population std of the 100 replicates (wave 0, one lane per window) ---- */
+  if (tid < FW_WPB && sh_row[tid] >= 0) {
+    const int wn = sh_n[tid];
+    const int wk = wn < FW_KTOP ? wn : FW_KTOP;
+    const int wbase = wn - wk;
+    const int widx = gd_perc_index(wn, perc);
+    const double wdelta = gd_perc_delta(wn, perc, widx);
+    const int64_t wg = g0 + tid;
+    if (sh_bad[tid] & FW_BAD_GENERAL) {
+      slow_list[atomicAdd(slow_count, 1u)] = (int32_t)wg;
     } else {
-      const int idx1 = (idx + 1 < n) ? idx + 1 : idx;
-      const double ws = gd_perc_mix(delta, sh_top[wl][idx - base], sh_top[wl][idx1 - base]);
-      const int64_t w = g - d.w_base;
+      const int widx1 = (widx + 1 < wn) ? widx + 1 : widx;
+      const double ws = gd_perc_mix(wdelta, sh_top[tid][widx - wbase], sh_top[tid][widx1 - wbase]);
+      const int64_t w = wg - d.w_base;
       scores[d.w_out + w] = ws;
-      stddev[d.w_out + w] = std_reverse_lds(sh_rep[wl]);
+      stddev[d.w_out + w] = std_reverse_lds(sh_rep[tid]);
     }
   }
 }

@@ -8,9 +8,10 @@ template <int OP>
 __global__ void k(unsigned *out, unsigned seed) {
   unsigned a[CH];
   double d[CH];
+  unsigned long long u[CH];
   const unsigned c = seed * 0x9E3779B9u | 1u;
   const double cd = 1.0000001;
-  for (int i = 0; i < CH; ++i) { a[i] = seed + threadIdx.x * 7 + i; d[i] = a[i]; }
+  for (int i = 0; i < CH; ++i) { a[i] = seed + threadIdx.x * 7 + i; d[i] = a[i]; u[i] = a[i]; }
   for (int it = 0; it < N_IT; ++it) {
 #pragma unroll
     for (int i = 0; i < CH; ++i) {
@@ -25,10 +26,19 @@ __global__ void k(unsigned *out, unsigned seed) {
       if (OP == 8) asm volatile("v_alignbit_b32 %0, %0, %1, 17" : "+v"(a[i]) : "v"(c));
       if (OP == 9) asm volatile("v_floor_f64 %0, %0" : "+v"(d[i]));
       if (OP == 10) asm volatile("v_cvt_f64_u32 %0, %1" : "=v"(d[i]) : "v"(a[i]));
+      if (OP == 11) asm volatile("v_lshrrev_b32 %0, 1, %0" : "+v"(a[i]));
+      if (OP == 12) asm volatile("v_sub_u32 %0, %0, %1" : "+v"(a[i]) : "v"(c));
+      if (OP == 13) asm volatile("v_max_i32 %0, %0, %1" : "+v"(a[i]) : "v"(c));
+      if (OP == 14) asm volatile("v_max3_u32 %0, %0, %1, %1" : "+v"(a[i]) : "v"(c));
+      if (OP == 15) asm volatile("v_add3_u32 %0, %0, %1, %1" : "+v"(a[i]) : "v"(c));
+      if (OP == 16) asm volatile("v_lshl_add_u32 %0, %0, 2, %1" : "+v"(a[i]) : "v"(c));
+      if (OP == 17) asm volatile("v_mad_u64_u32 %0, vcc, %1, %2, %0" : "+v"(u[i]) : "v"(a[i]), "v"(c) : "vcc");
+      if (OP == 18) asm volatile("v_cndmask_b32 %0, %0, %1, vcc" : "+v"(a[i]) : "v"(c));
+      if (OP == 19) asm volatile("v_and_b32 %0, %0, %1" : "+v"(a[i]) : "v"(c));
     }
   }
   unsigned s = 0;
-  for (int i = 0; i < CH; ++i) s += a[i] + (unsigned)d[i];
+  for (int i = 0; i < CH; ++i) s += a[i] + (unsigned)d[i] + (unsigned)u[i];
   out[blockIdx.x * blockDim.x + threadIdx.x] = s;
 }
 template <int OP>
@@ -60,5 +70,14 @@ int main() {
   printf("v_alignbit_b32   %.1f\n", run<8>(o));
   printf("v_floor_f64      %.1f\n", run<9>(o));
   printf("v_cvt_f64_u32    %.1f\n", run<10>(o));
+  printf("v_lshrrev_b32    %.1f\n", run<11>(o));
+  printf("v_sub_u32        %.1f\n", run<12>(o));
+  printf("v_max_i32        %.1f\n", run<13>(o));
+  printf("v_max3_u32       %.1f\n", run<14>(o));
+  printf("v_add3_u32       %.1f\n", run<15>(o));
+  printf("v_lshl_add_u32   %.1f\n", run<16>(o));
+  printf("v_mad_u64_u32    %.1f\n", run<17>(o));
+  printf("v_cndmask_b32    %.1f\n", run<18>(o));
+  printf("v_and_b32        %.1f\n", run<19>(o));
   return 0;
 }
