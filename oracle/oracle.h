@@ -25,4 +25,18 @@ int orc_fet_scan(const double *avals, const double *bvals, const int *apos, cons
                  double *scores, double *stddev);
 void orc_nrand48_stream(uint64_t x0, int n, long *out);
 
+/* CSS (css_oracle.c); matrices are dense row-major m*m */
+void orc_css_compare_all(const double *av, const double *bv, int asize, int bsize, int npos, double *D);
+int orc_css_fill_averages(double *D, int m);
+void orc_css_cmds(const double *D, int m, double *X, double *eig2);
+void orc_css_dist(const double *X, int m, double *S);
+double orc_css_score(const double *S, int m, const int *atr, const int *btr, int asize, int bsize);
+double orc_css_significance(const double *S, int m, int *tracks, int asize, int bsize, double score, int treshold,
+                            int runs, unsigned short st[3], int *nperm);
+int orc_css_window(const double *av, const double *bv, int asize, int bsize, int npos, int treshold, int runs,
+                   uint64_t state48, double *score, double *p, int *nperm);
+int orc_css_scan(const double *avals, const double *bvals, const int *apos, const int *bpos, int regend, int wsize,
+                 int wstep, int alen, int blen, int treshold, int runs, uint64_t seed, int serial, double *scores,
+                 double *p);
+
 #endif

@@ -11,6 +11,7 @@
  * fisher_exact_test() (cFisher.c:170-195) with a per-window nrand48 state.
  */
 #include <stdint.h>
+#include <math.h>
 #include <stdlib.h>
 
 #include "cFisher.h"
@@ -78,4 +79,10 @@ int ref_fet_scan_seeded(double *avals, double *bvals, int *apos, int *bpos, int 
   free(fs);
   free(sm);
   return 0;
+}
+
+/* -1.0 * log10(fet(table)) exactly as fisher_exact_test() computes a SNP's score (cFisher.c:182-183) */
+double ref_fet_score(int a, int b, int c, int d) {
+  int f[4] = {a, b, c, d}, tmp[4];
+  return -1.0 * log10(fet(f, tmp));
 }

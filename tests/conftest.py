@@ -107,3 +107,54 @@ def close(a, b, rel=1e-9, abs_=1e-12):
     both_nan = np.isnan(a) & np.isnan(b)
     ok = both_nan | (np.abs(a - b) <= rel * np.maximum(np.abs(a), np.abs(b)) + abs_)
     return bool(np.all(ok))
+
+
+SHIM_SRC = ROOT / "tests" / "host_shim" / "gd_common_shim.c"
+SHIM_LIB = ROOT / "tests" / ".build" / "libgdcommon_shim.so"
+
+
+@pytest.fixture(scope="session")
+def shim():
+    """gd_common.h (the kernels' scalar code) compiled for the host by gcc."""
+    SHIM_LIB.parent.mkdir(exist_ok=True)
+    subprocess.run(["gcc", "-O2", "-fPIC", "-shared", "-ffp-contract=off", "-I", str(PKG / "csrc"),
+                    "-o", str(SHIM_LIB), str(SHIM_SRC), "-lm"], check=True)
+    lib = ctypes.CDLL(str(SHIM_LIB))
+    C = ctypes
+    for fn in ("shim_fet", "shim_score"):
+        getattr(lib, fn).argtypes = [C.c_int] * 4
+        getattr(lib, fn).restype = C.c_double
+    lib.shim_log10.argtypes = [C.c_double]
+    lib.shim_log10.restype = C.c_double
+    lib.shim_binomial.argtypes = [C.c_uint64, C.c_uint64]
+    lib.shim_binomial.restype = C.c_uint64
+    lib.shim_window_state.argtypes = [C.c_uint64, C.c_uint64, C.c_int64]
+    lib.shim_window_state.restype = C.c_uint64
+    lib.shim_jump.argtypes = [C.c_uint64, C.c_uint64]
+    lib.shim_jump.restype = C.c_uint64
+    U32 = np.ctypeslib.ndpointer(np.uint32, flags="C")
+    lib.shim_stream.argtypes = [C.c_uint64, C.c_int, U32]
+    lib.shim_limit.argtypes = [C.c_uint32]
+    lib.shim_limit.restype = C.c_uint32
+    lib.shim_mod.argtypes = [C.c_uint32, U32, C.c_int, U32]
+    lib.shim_pair_index.argtypes = [C.c_int] * 3
+    return lib
+
+
+def load_scan_fixture(name):
+    """Decode tests/golden/fet_scan_<name>.npz into the reference's input arrays."""
+    z = np.load(GOLDEN / f"fet_scan_{name}.npz")
+    dec = {1: 3.0, 0: 0.0, -1: -3.0, -128: -10000.0}
+    def vals(code):
+        out = np.empty(code.shape, np.float64)
+        for k, v in dec.items():
+            out[code == k] = v
+        return out
+    a, b = int(z["asize"]), int(z["bsize"])
+    pos = z["pos"].astype(np.int32)
+    return dict(av=vals(z["acode"]), bv=vals(z["bcode"]), ap=np.repeat(pos, a), bp=np.repeat(pos, b),
+                regend=int(z["regend"]), wsize=int(z["wsize"]), wstep=int(z["wstep"]), perc=float(z["perc"]),
+                seed=int(z["seed"]), serial=bool(int(z["serial"])), scores=z["scores"], stddev=z["stddev"])
+
+
+SCAN_FIXTURES = ["10x10", "20x20", "7x13_w1000", "small_serial", "perc50"]

@@ -1,0 +1,27 @@
+/* Host build of csrc/gd_common.h (the device kernels' scalar code) for CPU unit
+ * tests: the same source, compiled by gcc with -ffp-contract=off. */
+#include "gd_common.h"
+
+static uint64_t shim_binom(int n, int k) { return gd_binomial_ref((uint64_t)(int64_t)n, (uint64_t)(int64_t)k); }
+#define SHIM_BINOM(n, k) shim_binom((n), (k))
+GD_DEFINE_FET(shim_fet_static, static, SHIM_BINOM)
+
+double shim_fet(int a, int b, int c, int d) { return shim_fet_static(a, b, c, d); }
+double shim_log10(double x) { return gd_log10_glibc(x); }
+double shim_score(int a, int b, int c, int d) { return gd_fet_score_from_p(shim_fet_static(a, b, c, d)); }
+uint64_t shim_binomial(uint64_t n, uint64_t k) { return gd_binomial_ref(n, k); }
+uint64_t shim_window_state(uint64_t seed, uint64_t stream, int64_t w) { return gd_window_state(seed, stream, w); }
+uint64_t shim_jump(uint64_t x, uint64_t k) { return gd_affine_apply(gd_lcg_jump(k), x); }
+void shim_stream(uint64_t x, int n, uint32_t *out) {
+  for (int i = 0; i < n; ++i) {
+    x = gd_lcg_next(x);
+    out[i] = gd_lcg_value(x);
+  }
+}
+uint32_t shim_limit(uint32_t n) { return gd_randint_make(n).limit; }
+/* r mod n through the magic-number path for every r in rs */
+void shim_mod(uint32_t n, const uint32_t *rs, int cnt, uint32_t *out) {
+  const gd_randint d = gd_randint_make(n);
+  for (int i = 0; i < cnt; ++i) out[i] = gd_randint_mod(&d, rs[i]);
+}
+int shim_pair_index(int maj, int mnr, int size) { return gd_pair_index(maj, mnr, size); }
