@@ -48,9 +48,11 @@ int gd_fet_window_fast_launch(const gd_chrom_dev *ch, int nchrom, const int32_t 
                               int blk_count, const int32_t *lo_a, const int32_t *hi_a, const int32_t *lo_b,
                               const double *snp_score, double perc, double *scores, double *stddev,
                               unsigned *flags, int32_t *slow_list, unsigned *slow_count, hipStream_t s);
-int gd_css_pipeline(struct gd_ctx *ctx, const gd_chrom_dev *d_ch, const std::vector<gd_chrom_dev> &h_ch,
-                    int64_t wtotal, const double *avals, const double *bvals, int wsize, int wstep, int treshold,
-                    int runs, double *scores, double *p, hipStream_t s);
+int gd_css_tier(int m);
+int gd_css_launch(int mp, const gd_chrom_dev *d_ch, int nchrom, const gd_css_planes *d_pl, uint32_t *planes,
+                  const int32_t *lo_a, const int32_t *hi_a, const int32_t *lo_b, const double *avals,
+                  const double *bvals, int64_t wtotal, int64_t max_rows_words, int treshold, int runs,
+                  double *scores, double *p, double *xbuf, uint8_t *status, unsigned *flags, hipStream_t s);
 int gd_synth_launch(int chrom, int nsnp, int asize, int bsize, uint64_t seed, const double *freq_table,
                     double *avals, double *bvals, int32_t *apos, int32_t *bpos, hipStream_t s);
 
@@ -486,9 +488,11 @@ static int css_scan_locked(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, cons
   for (float &m : g_stage_ms) m = 0.f;
   if (pl.wtotal == 0) return GD_OK;
   HIP_TRY(hipSetDevice(ctx->device));
+  /* pass 1: population sizes + window bounds; the CSS kernels are specialised on
+   * m = asize + bsize and the bit planes are sized by it, so read the sizes back */
   Carve cv{nullptr};
-  auto layout = [&](Carve &k, gd_chrom_dev **d_ch, unsigned **flags, int32_t **lo_a, int32_t **hi_a,
-                    int32_t **lo_b) {
+  auto layout1 = [&](Carve &k, gd_chrom_dev **d_ch, unsigned **flags, int32_t **lo_a, int32_t **hi_a,
+                     int32_t **lo_b) {
     *d_ch = k.take<gd_chrom_dev>(nchrom);
     *flags = k.take<unsigned>(16);
     *lo_a = k.take<int32_t>(pl.wtotal);
@@ -498,32 +502,97 @@ static int css_scan_locked(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, cons
   gd_chrom_dev *d_ch;
   unsigned *flags;
   int32_t *lo_a, *hi_a, *lo_b;
-  layout(cv, &d_ch, &flags, &lo_a, &hi_a, &lo_b);
+  layout1(cv, &d_ch, &flags, &lo_a, &hi_a, &lo_b);
   const size_t fixed = cv.off;
   if ((st = grow(&ctx->ws, &ctx->ws_cap, fixed))) return st;
-  Carve real{ctx->ws};
-  layout(real, &d_ch, &flags, &lo_a, &hi_a, &lo_b);
+  {
+    Carve real{ctx->ws};
+    layout1(real, &d_ch, &flags, &lo_a, &hi_a, &lo_b);
+  }
   HIP_TRY(hipMemcpyAsync(d_ch, pl.h.data(), sizeof(gd_chrom_dev) * nchrom, hipMemcpyHostToDevice, s));
   HIP_TRY(hipMemsetAsync(flags, 0, 16 * sizeof(unsigned), s));
   HIP_TRY(hipEventRecord(ctx->ev[0], s));
   hipLaunchKernelGGL(k_popsize, dim3(nchrom), dim3(64), 0, s, d_ch, apos, bpos, flags);
   {
     const int64_t mx = std::max(pl.max_alen, pl.max_blen) + 1;
-    const unsigned gx = (unsigned)std::min<int64_t>((mx + 255) / 256, 2048);
+    const unsigned gx = (unsigned)std::min<int64_t>((mx + 4095) / 4096, std::max(1, 8192 / nchrom));
     hipLaunchKernelGGL(k_bounds, dim3(gx, nchrom, 2), dim3(256), 0, s, d_ch, apos, bpos, wsize, wstep, lo_a,
                        hi_a, lo_b, flags);
   }
   HIP_TRY(hipGetLastError());
-  HIP_TRY(hipEventRecord(ctx->ev[1], s));
-  /* pull the population sizes back: the CSS kernels are specialised on m */
   HIP_TRY(hipMemcpyAsync(pl.h.data(), d_ch, sizeof(gd_chrom_dev) * nchrom, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipMemcpyAsync(ctx->h_flags, flags, 16 * sizeof(unsigned), hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
   if ((st = flags_to_status(ctx->h_flags[0]))) return st;
-  st = gd_css_pipeline(ctx, d_ch, pl.h, pl.wtotal, avals, bvals, wsize, wstep, treshold, runs, scores, p, s);
-  if (st) return st;
+
+  /* pass 2: bit planes, per-window MDS, permutations */
+  int mmax = 0;
+  int64_t words = 0, max_words = 1;
+  std::vector<gd_css_planes> hp(nchrom);
+  for (int c = 0; c < nchrom; ++c) {
+    const gd_chrom_dev &d = pl.h[c];
+    gd_css_planes &q = hp[c];
+    std::memset(&q, 0, sizeof q);
+    if (d.wend <= 0 || d.asize <= 0 || d.bsize <= 0) continue;
+    mmax = std::max(mmax, d.asize + d.bsize);
+    const int64_t wa = ((int64_t)d.alen / d.asize + 31) / 32 + 3, wb = ((int64_t)d.blen / d.bsize + 31) / 32 + 3;
+    if (wa > INT32_MAX || wb > INT32_MAX) return fail(GD_ERR_SIZE, "chromosome too long");
+    q.wa = (int32_t)wa;
+    q.wb = (int32_t)wb;
+    q.pa = words;
+    words += (2 * (int64_t)d.asize + 1) * wa;
+    q.pb = words;
+    words += (2 * (int64_t)d.bsize + 1) * wb;
+    max_words = std::max(max_words, std::max(wa * d.asize, wb * d.bsize));
+  }
+  const int mp = gd_css_tier(mmax);
+  if (mp == 0) return fail(GD_ERR_SIZE, "asize + bsize above the largest supported CSS tier (96)");
+  const bool perms = runs > 0 && treshold > 0;
+  auto layout2 = [&](Carve &k, gd_css_planes **d_pl, uint32_t **planes, double **xbuf, uint8_t **status) {
+    layout1(k, &d_ch, &flags, &lo_a, &hi_a, &lo_b);
+    *d_pl = k.take<gd_css_planes>(nchrom);
+    *planes = k.take<uint32_t>(std::max<int64_t>(words, 1));
+    *xbuf = k.take<double>(perms ? pl.wtotal * 2 * mp : 1);
+    *status = k.take<uint8_t>(perms ? pl.wtotal : 1);
+  };
+  gd_css_planes *d_pl;
+  uint32_t *planes;
+  double *xbuf;
+  uint8_t *status;
+  Carve cv2{nullptr};
+  layout2(cv2, &d_pl, &planes, &xbuf, &status);
+  if (cv2.off > ctx->ws_cap) {
+    /* growing reallocates: keep the pass-1 results (descriptors, flags, bounds) */
+    char *old = ctx->ws;
+    ctx->ws = nullptr;
+    ctx->ws_cap = 0;
+    if ((st = grow(&ctx->ws, &ctx->ws_cap, cv2.off))) {
+      (void)hipFree(old);
+      return st;
+    }
+    HIP_TRY(hipMemcpyAsync(ctx->ws, old, fixed, hipMemcpyDeviceToDevice, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    (void)hipFree(old);
+  }
+  {
+    Carve real{ctx->ws};
+    layout2(real, &d_pl, &planes, &xbuf, &status);
+  }
+  HIP_TRY(hipMemcpyAsync(d_ch, pl.h.data(), sizeof(gd_chrom_dev) * nchrom, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(d_pl, hp.data(), sizeof(gd_css_planes) * nchrom, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemsetAsync(planes, 0, sizeof(uint32_t) * std::max<int64_t>(words, 1), s));
+  if (perms) HIP_TRY(hipMemsetAsync(status, 0, pl.wtotal, s));
+  HIP_TRY(hipEventRecord(ctx->ev[1], s));
+  st = gd_css_launch(mp, d_ch, nchrom, d_pl, planes, lo_a, hi_a, lo_b, avals, bvals, pl.wtotal, max_words,
+                     treshold, runs, scores, p, xbuf, status, flags, s);
+  if (st) return fail(st, "CSS kernel launch failed");
+  HIP_TRY(hipEventRecord(ctx->ev[3], s));
   HIP_TRY(hipMemcpyAsync(ctx->h_flags, flags, 16 * sizeof(unsigned), hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
+  float ms;
+  if (hipEventElapsedTime(&ms, ctx->ev[0], ctx->ev[1]) == hipSuccess) g_stage_ms[GD_STAGE_MEM] = ms;
+  if (hipEventElapsedTime(&ms, ctx->ev[1], ctx->ev[3]) == hipSuccess) g_stage_ms[GD_STAGE_WINDOW] = ms;
+  if (hipEventElapsedTime(&ms, ctx->ev[0], ctx->ev[3]) == hipSuccess) g_stage_ms[GD_STAGE_TOTAL] = ms;
   return flags_to_status(ctx->h_flags[0]);
 }
 

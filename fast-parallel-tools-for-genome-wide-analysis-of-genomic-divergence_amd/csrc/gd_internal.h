@@ -36,3 +36,12 @@ typedef struct gd_chrom_dev {
 #define GD_MAX_GROUPS 4 /* chromosome groups pipelined across two streams */
 #define GD_LUT_CAP (1 << 22) /* FET score-table entries (32 MB): up to ~62+62 individuals */
 #define GD_NREP 100 /* bootstrap replicates (cFisher.c:62) */
+
+/* CSS bit planes of one chromosome (word offsets into the plane buffer).  Pop A:
+ * individual i's "== 3" plane at pa + 2i*wa, its "== -3" plane at pa + (2i+1)*wa,
+ * the per-row "irregular value" plane at pa + 2*asize*wa; pop B likewise.  A plane
+ * holds one bit per SNP row plus 3 zero words of padding. */
+typedef struct gd_css_planes {
+  int64_t pa, pb;
+  int32_t wa, wb;
+} gd_css_planes;

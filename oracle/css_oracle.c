@@ -27,6 +27,7 @@
  * test_calc_dist, test_cmds, test_css) in tests/test_oracle_css.py.
  */
 #define _DEFAULT_SOURCE
+#include <float.h>
 #include <math.h>
 #include <stdint.h>
 #include <stdlib.h>
@@ -81,25 +82,31 @@ int orc_css_fill_averages(double *D, int m) {
   return 1;
 }
 
-/* cyclic Jacobi: A (m*m, destroyed) -> eigenvalues w, eigenvectors in the columns of V */
+/* cyclic Jacobi (the Numerical Recipes "jacobi" thresholds): A (m*m, destroyed)
+ * -> eigenvalues w, eigenvectors in the columns of V.  Off-diagonal entries that
+ * no longer change the diagonal in floating point are zeroed, so the sweep loop
+ * ends with an exactly diagonal A (typically 6-10 sweeps). */
 static void orc_jacobi(double *A, int m, double *w, double *V) {
   int i, j, k, p, sweep;
   for (i = 0; i < m; i++)
     for (j = 0; j < m; j++) V[i * m + j] = (i == j);
   for (sweep = 0; sweep < 100; sweep++) {
-    double off = 0, tot = 0;
-    for (i = 0; i < m; i++)
-      for (j = 0; j < m; j++) {
-        tot += A[i * m + j] * A[i * m + j];
-        if (i != j) off += A[i * m + j] * A[i * m + j];
-      }
-    if (off <= 1e-32 * tot || off == 0) break;
+    double off = 0, thresh;
+    for (p = 0; p < m - 1; p++)
+      for (k = p + 1; k < m; k++) off += fabs(A[p * m + k]);
+    if (off == 0.0) break;
+    thresh = sweep < 3 ? 0.2 * off / (m * m) : 0.0;
     for (p = 0; p < m - 1; p++)
       for (k = p + 1; k < m; k++) {
-        double apq = A[p * m + k], app, aqq, theta, t, c, s;
-        if (fabs(apq) < 1e-300) continue;
+        double apq = A[p * m + k], app, aqq, theta, t, c, s, g = 100.0 * fabs(apq);
         app = A[p * m + p];
         aqq = A[k * m + k];
+        if (sweep > 3 && fabs(app) + g == fabs(app) && fabs(aqq) + g == fabs(aqq)) {
+          A[p * m + k] = 0.0;
+          A[k * m + p] = 0.0;
+          continue;
+        }
+        if (fabs(apq) <= thresh || apq == 0.0) continue;
         theta = (aqq - app) / (2 * apq);
         t = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1));
         c = 1 / sqrt(t * t + 1);
@@ -114,6 +121,8 @@ static void orc_jacobi(double *A, int m, double *w, double *V) {
           A[p * m + i] = c * api - s * aqi;
           A[k * m + i] = s * api + c * aqi;
         }
+        A[p * m + k] = 0.0;
+        A[k * m + p] = 0.0;
         for (i = 0; i < m; i++) {
           double vip = V[i * m + p], viq = V[i * m + k];
           V[i * m + p] = c * vip - s * viq;
@@ -129,7 +138,7 @@ void orc_css_cmds(const double *D, int m, double *X, double *eig2) {
   double *B = malloc(sizeof(double) * m * m), *Z = malloc(sizeof(double) * m * m);
   double *T = malloc(sizeof(double) * m * m), *V = malloc(sizeof(double) * m * m), *w = malloc(sizeof(double) * m);
   int i, j, k, i0 = 0, i1 = 1;
-  double L0, L1;
+  double L0, L1, zero_tol;
   for (i = 0; i < m * m; i++) B[i] = D[i] * D[i];
   for (i = m; i--;)
     for (j = m; j--;) Z[i * m + j] = (i != j) ? -1.0 / m : (m - 1) / (m * 1.0);
@@ -147,7 +156,20 @@ void orc_css_cmds(const double *D, int m, double *X, double *eig2) {
     }
   for (i = m; i--;)
     for (j = m; j--;) B[i * m + j] *= -0.5;
+  {
+    /* eigenvalues within rounding of 0 are 0 (see below) */
+    double fro = 0;
+    for (i = 0; i < m * m; i++) fro += B[i] * B[i];
+    zero_tol = 64.0 * m * DBL_EPSILON * sqrt(fro);
+  }
   orc_jacobi(B, m, w, V);
+  /* Documented deviation: B = -1/2 Z D2 Z always has the eigenvalue 0 (eigenvector
+   * 1), so a window of rank <= 1 has lambda_2 = 0 exactly and the reference's
+   * sqrt(lambda_2) is NaN or finite depending on the solver's rounding (GSL is not
+   * available to pin it).  Both the oracle and the HIP kernel treat |lambda| <=
+   * 64 m eps ||B||_F as 0, i.e. the finite outcome. */
+  for (i = 0; i < m; i++)
+    if (fabs(w[i]) <= zero_tol) w[i] = 0.0;
   /* the two largest eigenvalues, first occurrence on ties (a stable descending sort) */
   for (i = 0; i < m; i++)
     if (w[i] > w[i0]) i0 = i;

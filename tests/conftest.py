@@ -68,6 +68,8 @@ def oracle():
     lib.orc_percentile.argtypes = [DP, C.c_int, C.c_double]
     lib.orc_percentile.restype = C.c_double
     lib.orc_population_size.argtypes = [IP, C.c_int]
+    lib.orc_css_scan.argtypes = [DP, DP, IP, IP, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                 C.c_uint64, C.c_int, DP, DP]
     return lib
 
 
@@ -78,6 +80,17 @@ def oracle_fet_scan(orc, av, bv, ap, bp, regend, wsize=2500, wstep=500, perc=0.9
     rc = orc.orc_fet_scan(av, bv, ap, bp, regend, wsize, wstep, len(av), len(bv), perc, seed, int(serial), s, d)
     assert rc == 0
     return s, d
+
+
+def oracle_css_scan(orc, av, bv, ap, bp, regend, wsize=2500, wstep=500, treshold=10, runs=0, seed=20261015,
+                    serial=False):
+    n = regend // wstep
+    s = np.zeros(n)
+    p = np.zeros(n)
+    rc = orc.orc_css_scan(av, bv, ap, bp, regend, wsize, wstep, len(av), len(bv), treshold, runs, seed, int(serial),
+                          s, p)
+    assert rc == 0
+    return s, p
 
 
 @pytest.fixture(scope="session")
