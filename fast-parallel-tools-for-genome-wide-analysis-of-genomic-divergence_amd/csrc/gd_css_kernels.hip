@@ -29,12 +29,30 @@
 
 #include <cfloat>
 #include <climits>
+#include <cstdio>
 #include <cstdlib>
 #include <vector>
 
 #include "../../include/gdscan.h"
 #include "gd_common.h"
 #include "gd_internal.h"
+
+#ifdef GD_CSS_PROFILE
+/* diagnostics build only: shader-clock cycles per phase summed over windows (lane 0) */
+__device__ unsigned long long g_css_prof[8];
+#define CSS_PROF_INIT uint64_t prof_t = __builtin_readcyclecounter()
+#define CSS_PROF(ph)                                                  \
+  do {                                                                \
+    if (threadIdx.x == 0) {                                           \
+      const uint64_t t_ = __builtin_readcyclecounter();              \
+      atomicAdd(&g_css_prof[ph], (unsigned long long)(t_ - prof_t)); \
+      prof_t = t_;                                                    \
+    }                                                                 \
+  } while (0)
+#else
+#define CSS_PROF_INIT
+#define CSS_PROF(ph)
+#endif
 
 namespace {
 
@@ -52,100 +70,138 @@ __device__ __forceinline__ uint64_t plane_bits64(const uint32_t *pl, int64_t bit
  * register-resident matrix row); loops issue their loads in groups of 8. */
 #define CSS_GROUP_FENCE(j) \
   if (((j) & 7) == 7) asm volatile("" ::: "memory")
+/* Pins a value: everything producing it happens before this point and no later
+ * LDS load moves above it.  Used once per 8-column group so a group's broadcast
+ * loads are consumed before the next group's are issued. */
+#define CSS_PIN(x) asm volatile("" : "+v"(x)::"memory")
 
 /* A copy of x the compiler cannot see through: per-column predicates built from it
  * (j < m, j vs lane) are materialised inside the loop that uses them instead of
  * being hoisted out of the window loop as one live SGPR mask per column. */
 #define CSS_OPAQUE_S(x) asm volatile("" : "+s"(x))
 #define CSS_OPAQUE_V(x) asm volatile("" : "+v"(x))
+/* the same for a whole register-resident row: values derived from it before this
+ * point (compare masks, partial products) cannot be reused after it */
+#define CSS_OPAQUE_ROW(R)                                   \
+  do {                                                      \
+    _Pragma("unroll") for (int j_ = 0; j_ < MP; ++j_) CSS_OPAQUE_V(R[j_]); \
+  } while (0)
 
 /* x86 cvttsd2si: NaN and out-of-range values give INT_MIN */
 __device__ __forceinline__ double x86_int(double v) {
   return (v > -2147483649.0 && v < 2147483648.0) ? (double)(int)v : (double)INT_MIN;
 }
 
-/* wave64 reductions; the result is lane 0's, so every lane holds the same bits */
-__device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
-  return __shfl(v, 0);
+/* wave64 reductions over DPP (quad_perm, row_ror, row_bcast): the total lands in
+ * lane 63 and is read back as a wave-uniform scalar, so every lane holds the same
+ * bits and control flow that depends on it stays uniform. */
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ uint32_t dpp32(uint32_t v, uint32_t ident) {
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)ident, (int)v, CTRL, ROWMASK, 0xF, false);
 }
-__device__ __forceinline__ int wave_sum_i(int v) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
-  return v;
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ double dpp64(double v, double ident) {
+  const uint64_t u = __builtin_bit_cast(uint64_t, v), id = __builtin_bit_cast(uint64_t, ident);
+  const uint32_t lo = dpp32<CTRL, ROWMASK>((uint32_t)u, (uint32_t)id);
+  const uint32_t hi = dpp32<CTRL, ROWMASK>((uint32_t)(u >> 32), (uint32_t)(id >> 32));
+  return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
 }
-__device__ __forceinline__ double wave_min(double v) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v = fmin(v, __shfl_xor(v, o));
-  return v;
+__device__ __forceinline__ double lane63(double v) {
+  const uint64_t u = __builtin_bit_cast(uint64_t, v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, 63);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), 63);
+  return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
 }
-__device__ __forceinline__ double wave_max(double v) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v = fmax(v, __shfl_xor(v, o));
-  return v;
+struct OpSum {
+  static __device__ __forceinline__ double id() { return 0.0; }
+  static __device__ __forceinline__ double op(double x, double y) { return x + y; }
+};
+struct OpMin {
+  static __device__ __forceinline__ double id() { return __builtin_huge_val(); }
+  static __device__ __forceinline__ double op(double x, double y) { return fmin(x, y); }
+};
+struct OpMax {
+  static __device__ __forceinline__ double id() { return -__builtin_huge_val(); }
+  static __device__ __forceinline__ double op(double x, double y) { return fmax(x, y); }
+};
+template <class Op>
+__device__ __forceinline__ double wave_reduce(double v) {
+  const double e = Op::id();
+  v = Op::op(v, dpp64<0xB1, 0xF>(v, e));
+  v = Op::op(v, dpp64<0x4E, 0xF>(v, e));
+  v = Op::op(v, dpp64<0x124, 0xF>(v, e));
+  v = Op::op(v, dpp64<0x128, 0xF>(v, e));
+  v = Op::op(v, dpp64<0x142, 0xA>(v, e));
+  v = Op::op(v, dpp64<0x143, 0xC>(v, e));
+  return lane63(v);
+}
+/* two sums at once (independent DPP chains interleave) */
+__device__ __forceinline__ void wave_sum2(double &a, double &b) {
+  a += dpp64<0xB1, 0xF>(a, 0.0);
+  b += dpp64<0xB1, 0xF>(b, 0.0);
+  a += dpp64<0x4E, 0xF>(a, 0.0);
+  b += dpp64<0x4E, 0xF>(b, 0.0);
+  a += dpp64<0x124, 0xF>(a, 0.0);
+  b += dpp64<0x124, 0xF>(b, 0.0);
+  a += dpp64<0x128, 0xF>(a, 0.0);
+  b += dpp64<0x128, 0xF>(b, 0.0);
+  a += dpp64<0x142, 0xA>(a, 0.0);
+  b += dpp64<0x142, 0xA>(b, 0.0);
+  a += dpp64<0x143, 0xC>(a, 0.0);
+  b += dpp64<0x143, 0xC>(b, 0.0);
+  a = lane63(a);
+  b = lane63(b);
 }
 
-/* block reductions over NW waves; red must hold NW doubles */
+/* block reductions over NW waves; red must hold 2*NW doubles */
+template <int NW, class Op>
+__device__ __forceinline__ double block_reduce(double v, double *red) {
+  v = wave_reduce<Op>(v);
+  if constexpr (NW == 1) {
+    return v;
+  } else {
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    double s = red[0];
+#pragma unroll
+    for (int k = 1; k < NW; ++k) s = Op::op(s, red[k]);
+    return s;
+  }
+}
 template <int NW>
 __device__ __forceinline__ double block_sum(double v, double *red) {
-  v = wave_sum(v);
-  if constexpr (NW == 1) {
-    return v;
-  } else {
-    __syncthreads();
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
-    __syncthreads();
-    double s = red[0];
-#pragma unroll
-    for (int k = 1; k < NW; ++k) s += red[k];
-    return s;
-  }
+  return block_reduce<NW, OpSum>(v, red);
 }
 template <int NW>
-__device__ __forceinline__ int block_sum_i(int v, double *red) {
-  v = wave_sum_i(v);
-  if constexpr (NW == 1) {
-    return v;
-  } else {
+__device__ __forceinline__ void block_sum2(double &a, double &b, double *red) {
+  wave_sum2(a, b);
+  if constexpr (NW > 1) {
     __syncthreads();
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = (double)v;
+    if ((threadIdx.x & 63) == 0) {
+      red[threadIdx.x >> 6] = a;
+      red[NW + (threadIdx.x >> 6)] = b;
+    }
     __syncthreads();
-    int s = 0;
+    double sa = red[0], sb = red[NW];
 #pragma unroll
-    for (int k = 0; k < NW; ++k) s += (int)red[k];
-    return s;
+    for (int k = 1; k < NW; ++k) {
+      sa += red[k];
+      sb += red[NW + k];
+    }
+    a = sa;
+    b = sb;
   }
 }
-template <int NW>
-__device__ __forceinline__ double block_min(double v, double *red) {
-  v = wave_min(v);
-  if constexpr (NW == 1) {
-    return v;
-  } else {
-    __syncthreads();
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
-    __syncthreads();
-    double s = red[0];
-#pragma unroll
-    for (int k = 1; k < NW; ++k) s = fmin(s, red[k]);
-    return s;
-  }
-}
-template <int NW>
-__device__ __forceinline__ double block_max(double v, double *red) {
-  v = wave_max(v);
-  if constexpr (NW == 1) {
-    return v;
-  } else {
-    __syncthreads();
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
-    __syncthreads();
-    double s = red[0];
-#pragma unroll
-    for (int k = 1; k < NW; ++k) s = fmax(s, red[k]);
-    return s;
-  }
+
+/* 1/x to full precision: hardware estimate + two Newton steps (no IEEE division
+ * sequence; used only off the bit-exact path) */
+__device__ __forceinline__ double fast_rcp(double x) {
+  double r = __builtin_amdgcn_rcp(x);
+  double e = fma(-x, r, 1.0);
+  r = fma(r, e, r);
+  e = fma(-x, r, 1.0);
+  return fma(r, e, r);
 }
 
 __device__ __forceinline__ int chrom_of(const gd_chrom_dev *ch, int nchrom, int64_t w) {
@@ -171,25 +227,19 @@ __device__ __forceinline__ double xdist(const double *X, int i, int j) {
 template <int NW, class Dist>
 __device__ __forceinline__ double css_score(const int *tracks, int a, int b, Dist dist, double *red) {
   constexpr int NT = 64 * NW;
-  const int t = threadIdx.x, ab = a * b;
+  const int t = threadIdx.x, ab = a * b, m = a + b;
   const float invb = 1.0f / (float)b;
-  double bet = 0;
+  double bet = 0, win = 0;
   for (int q = t; q < ab; q += NT) {
     const int ii = (int)(((float)q + 0.5f) * invb); /* exact for q < 2^14 */
     const int jj = q - ii * b;
     bet += dist(tracks[ii], tracks[a + jj]);
   }
-  const int m = a + b;
-  double ad = 0, bd = 0;
-  if (t < a - 1) ad = dist(tracks[t], tracks[t + 1]);
-  if (t >= a && t < m - 1) bd = dist(tracks[t], tracks[t + 1]);
-  bet = block_sum<NW>(bet, red);
-  ad = block_sum<NW>(ad, red);
-  bd = block_sum<NW>(bd, red);
-  bet = bet / (a * b);
-  if (a > 1) ad = ad / (a * a * (a - 1));
-  if (b > 1) bd = bd / (b * b * (b - 1));
-  return bet - (a + b) * (ad + bd);
+  /* consecutive pairs only (Q8), each pre-divided by its group's a^2 (a-1) */
+  if (t < a - 1) win = dist(tracks[t], tracks[t + 1]) / (double)(a * a * (a - 1));
+  if (t >= a && t < m - 1) win = dist(tracks[t], tracks[t + 1]) / (double)(b * b * (b - 1));
+  block_sum2<NW>(bet, win, red);
+  return bet / (a * b) - (a + b) * win;
 }
 
 }  // namespace
@@ -241,7 +291,9 @@ __global__ void __launch_bounds__(64 * ((MP + 63) / 64))
   constexpr int NW = (MP + 63) / 64;
   __shared__ double s_row[MP + 2];
   __shared__ double s_v[MP], s_w[MP];
-  __shared__ double s_d[MP], s_e[MP], s_e2[MP], s_tau[MP];
+  __shared__ __attribute__((aligned(16))) double s_d[MP + 4];
+  __shared__ __attribute__((aligned(16))) double s_e2[MP + 4];
+  __shared__ double s_e[MP], s_tau[MP];
   __shared__ uint64_t s_mask[2 * MP];
   __shared__ double s_vals[MP];
   __shared__ double s_y[2][MP];
@@ -250,13 +302,16 @@ __global__ void __launch_bounds__(64 * ((MP + 63) / 64))
   __shared__ double s_x[2 * MP];
   __shared__ int s_tr[MP];
   __shared__ double s_lam[2];
-  __shared__ double s_red[NW];
+  __shared__ double s_red[2 * NW];
 
   const int i = threadIdx.x;
   const int ii = i < MP ? i : MP - 1; /* clamped LDS index for lanes past MP */
   if (i < MP) s_tr[i] = i;
 
-  for (int64_t w = blockIdx.x; w < wtotal; w += gridDim.x) {
+  /* one workgroup per window (no persistent loop: hoisting per-lane invariants out of
+   * a window loop costs ~100 VGPRs and halves the occupancy) */
+  for (int64_t w = blockIdx.x; w < wtotal; w += wtotal) {
+    CSS_PROF_INIT;
     const int c = chrom_of(ch, nchrom, w);
     const gd_chrom_dev &d = ch[c];
     const int a = d.asize, b = d.bsize, m = a + b;
@@ -318,7 +373,10 @@ __global__ void __launch_bounds__(64 * ((MP + 63) / 64))
           for (int j = 0; j < MP; ++j) {
             const uint64_t Pj = s_mask[2 * j], Nj = s_mask[2 * j + 1];
             acc[j] += __popcll(Pi & Nj) + __popcll(Ni & Pj);
-            CSS_GROUP_FENCE(j);
+            if ((j & 7) == 7) {
+#pragma unroll
+              for (int u = j - 7; u <= j; ++u) CSS_PIN(acc[u]);
+            }
           }
         }
       } else {
@@ -352,6 +410,7 @@ __global__ void __launch_bounds__(64 * ((MP + 63) / 64))
       for (int j = 0; j < MP; ++j) A[j] = (row && j < mo) ? (double)acc[j] : 0.0;
     }
 
+    CSS_PROF(0);
     /* ---- fill_averages: entries < 1e-5 (diagonal included) count as unknown */
     {
       int unval = 0;
@@ -367,24 +426,29 @@ __global__ void __launch_bounds__(64 * ((MP + 63) / 64))
             sum += A[j];
         }
       }
-      unval = block_sum_i<NW>(unval, s_red);
-      sum = block_sum<NW>(sum, s_red); /* sums of integers: exact in any order */
+      double unv = (double)unval;
+      block_sum2<NW>(unv, sum, s_red); /* sums of integers: exact in any order */
+      unval = (int)unv;
       const int tot = m * m;
       if (unval > tot / 2) continue; /* discarded window: outputs untouched */
       const double avg = sum / tot;
-      CSS_OPAQUE_S(mo);
+      /* D holds non-negative integer counts, so "< 1e-5" is "== 0" and the fill is
+       * A + avg (1 - min(A, 1)), exact and mask-free (no per-column compare results
+       * kept alive across the reduction); padding columns are re-zeroed below */
+      CSS_OPAQUE_ROW(A);
 #pragma unroll
-      for (int j = 0; j < MP; ++j)
-        if (row && j < mo && A[j] < 0.00001) A[j] = avg;
+      for (int j = 0; j < MP; ++j) A[j] = fma(avg, 1.0 - fmin(A[j], 1.0), A[j]);
     }
 
     /* ---- B = -1/2 Z (D o D) Z, Z = I - 11^T/m, by double centering */
     double zero_tol;
     {
       double rs = 0;
+      int mo = m;
+      CSS_OPAQUE_S(mo);
 #pragma unroll
       for (int j = 0; j < MP; ++j) {
-        A[j] = A[j] * A[j];
+        A[j] = (row && j < mo) ? A[j] * A[j] : 0.0;
         rs += A[j];
       }
       const double ri = row ? rs / m : 0.0;
@@ -392,10 +456,15 @@ __global__ void __launch_bounds__(64 * ((MP + 63) / 64))
       if (i < MP) s_v[i] = ri;
       const double g = block_sum<NW>(ri, s_red) / m;
       __syncthreads();
-      int mo = m;
       CSS_OPAQUE_S(mo);
 #pragma unroll
-      for (int j = 0; j < MP; ++j) A[j] = (row && j < mo) ? -0.5 * ((A[j] - (ri + s_v[j])) + g) : 0.0;
+      for (int j = 0; j < MP; ++j) {
+        A[j] = (row && j < mo) ? -0.5 * ((A[j] - (ri + s_v[j])) + g) : 0.0;
+        if ((j & 7) == 7) {
+#pragma unroll
+          for (int u = j - 7; u <= j; ++u) CSS_PIN(A[u]);
+        }
+      }
       double f2 = 0;
 #pragma unroll
       for (int j = 0; j < MP; ++j) f2 = fma(A[j], A[j], f2);
@@ -403,87 +472,119 @@ __global__ void __launch_bounds__(64 * ((MP + 63) / 64))
       zero_tol = 64.0 * m * DBL_EPSILON * sqrt(block_sum<NW>(f2, s_red));
     }
 
+    CSS_PROF(1);
     /* ---- Householder tridiagonalisation (LAPACK dsytd2, lower).  Column k of the
      * trailing matrix is read from row k (symmetry); after step k the dead column k
      * of each row holds that row's element of the reflector v_k. */
     for (int k = 0; k < m; ++k) {
       __syncthreads();
+      /* Columns are handled in blocks of 8; blocks entirely left of k are dead
+       * (their v and w entries are 0) and skipped by a uniform branch.  Lane k
+       * publishes x = row k right of the diagonal (zeros at j <= k) and d_k. */
       if (i == k) {
 #pragma unroll
-        for (int j = 0; j < MP; ++j) s_row[j] = A[j];
+        for (int jb = 0; jb < MP / 8; ++jb)
+          if (8 * jb + 7 >= k) {
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+              const int j = 8 * jb + u;
+              s_row[j] = j > k ? A[j] : 0.0;
+              if (j == k) s_d[k] = A[j];
+            }
+          }
       }
       __syncthreads();
       if (k >= m - 2) {
-        if (i == 0) {
-          s_d[k] = s_row[k];
-          if (k == m - 2) s_e[k] = s_row[k + 1];
-        }
+        if (i == 0 && k == m - 2) s_e[k] = s_row[k + 1];
         continue;
       }
       const double xi = (i > k + 1 && row) ? s_row[ii] : 0.0;
       const double alpha = s_row[k + 1];
+      /* A x and A e_{k+1} need only x, so they overlap the norm reduction */
+      double p0 = 0, p1 = 0, ak1 = 0;
+#pragma unroll
+      for (int jb = 0; jb < MP / 8; ++jb) {
+        if (8 * jb + 7 > k) {
+#pragma unroll
+          for (int u = 0; u < 8; u += 2) {
+            p0 = fma(A[8 * jb + u], s_row[8 * jb + u], p0);
+            p1 = fma(A[8 * jb + u + 1], s_row[8 * jb + u + 1], p1);
+          }
+          CSS_PIN(p0);
+          CSS_PIN(p1);
+        }
+        if (((k + 1) >> 3) == jb) {
+#pragma unroll
+          for (int u = 0; u < 8; ++u) ak1 = (8 * jb + u == k + 1) ? A[8 * jb + u] : ak1;
+        }
+      }
       const double sigma = block_sum<NW>(xi * xi, s_red);
       double tau = 0.0, beta = alpha, scale = 0.0;
       if (sigma != 0.0) {
         beta = -copysign(sqrt(alpha * alpha + sigma), alpha);
-        tau = (beta - alpha) / beta;
-        scale = 1.0 / (alpha - beta);
+        tau = (beta - alpha) * fast_rcp(beta);
+        scale = fast_rcp(alpha - beta);
       }
+      /* v = scale (x - beta e_{k+1}), v_{k+1} = 1;  p = tau A v */
       const double vi = (i == k + 1) ? 1.0 : xi * scale;
+      const double pi = (i > k && row) ? (tau * scale) * fma(-beta, ak1, p0 + p1) : 0.0;
+      const double K = -0.5 * tau * block_sum<NW>(pi * vi, s_red);
+      const double wi = fma(K, vi, pi);
       if (i == 0) {
-        s_d[k] = s_row[k];
         s_e[k] = beta;
         s_tau[k] = tau;
       }
-      if (i < MP) s_v[i] = vi;
-      __syncthreads();
-      double p0 = 0, p1 = 0, p2 = 0, p3 = 0;
-#pragma unroll
-      for (int j = 0; j < MP; j += 4) {
-        p0 = fma(A[j], s_v[j], p0);
-        if (j + 1 < MP) p1 = fma(A[j + 1], s_v[j + 1], p1);
-        if (j + 2 < MP) p2 = fma(A[j + 2], s_v[j + 2], p2);
-        if (j + 3 < MP) p3 = fma(A[j + 3], s_v[j + 3], p3);
-        CSS_GROUP_FENCE(j + 4);
+      if (i < MP) {
+        s_v[i] = vi;
+        s_w[i] = wi;
       }
-      const double pi = (i > k && row) ? tau * ((p0 + p1) + (p2 + p3)) : 0.0;
-      const double K = -0.5 * tau * block_sum<NW>(pi * vi, s_red);
-      const double wi = pi + K * vi;
-      if (i < MP) s_w[i] = wi;
       __syncthreads();
 #pragma unroll
-      for (int j = 0; j < MP; ++j) {
-        A[j] = fma(-vi, s_w[j], fma(-wi, s_v[j], A[j]));
-        CSS_GROUP_FENCE(j);
-      }
+      for (int jb = 0; jb < MP / 8; ++jb) {
+        if (8 * jb + 7 > k) {
 #pragma unroll
-      for (int j = 0; j < MP; ++j) A[j] = (j == k) ? vi : A[j];
+          for (int u = 0; u < 8; ++u) {
+            const int j = 8 * jb + u;
+            A[j] = fma(-vi, s_w[j], fma(-wi, s_v[j], A[j]));
+          }
+#pragma unroll
+          for (int u = 0; u < 8; ++u) CSS_PIN(A[8 * jb + u]);
+        }
+        /* stash v_k in the dead column k */
+        if ((k >> 3) == jb) {
+#pragma unroll
+          for (int u = 0; u < 8; ++u) A[8 * jb + u] = (8 * jb + u == k) ? vi : A[8 * jb + u];
+        }
+      }
     }
     __syncthreads();
 
+    CSS_PROF(2);
     /* ---- the two largest eigenvalues of T: Gershgorin bounds, then 33-section
-     * Sturm-count bisection, one half-wave per eigenvalue */
-    double glo, ghi, pivmin;
+     * bisection, one half-wave per eigenvalue.  Sturm counts come from the sign
+     * changes of the leading principal minors p_k(x) (three-term recurrence,
+     * rescaled every 4 steps): no division on the serial chain. */
+    double glo, ghi;
     {
-      double lo = DBL_MAX, hi = -DBL_MAX, e2m = 0;
+      double lo = DBL_MAX, hi = -DBL_MAX;
       if (row) {
         const double r = (i > 0 ? fabs(s_e[i - 1]) : 0.0) + (i < m - 1 ? fabs(s_e[i]) : 0.0);
         lo = s_d[i] - r;
         hi = s_d[i] + r;
-        if (i < m - 1) {
-          const double e2 = s_e[i] * s_e[i];
-          s_e2[i] = e2;
-          e2m = e2;
-        }
       }
-      glo = block_min<NW>(lo, s_red);
-      ghi = block_max<NW>(hi, s_red);
-      e2m = block_max<NW>(e2m, s_red);
-      pivmin = DBL_MIN * fmax(1.0, e2m);
-      const double tn = fmax(fabs(glo), fabs(ghi));
-      glo -= 2.0 * DBL_EPSILON * tn * m + 2.0 * pivmin;
-      ghi += 2.0 * DBL_EPSILON * tn * m + 2.0 * pivmin;
+      if (i < MP + 4) {
+        /* Sturm arrays: s_e2[k] = e_{k-1}^2 (s_e2[0] = 0); entries m..m4 are a
+         * decoupled tail far above the spectrum (no sign changes) */
+        s_e2[i] = (i >= 1 && i < m) ? s_e[i - 1] * s_e[i - 1] : 0.0;
+      }
+      glo = block_reduce<NW, OpMin>(lo, s_red);
+      ghi = block_reduce<NW, OpMax>(hi, s_red);
+      const double pad = 2.0 * DBL_EPSILON * fmax(fabs(glo), fabs(ghi)) * m + DBL_MIN;
+      glo -= pad;
+      ghi += pad;
+      if (i >= m && i < MP + 4) s_d[i] = 2.0 * fabs(ghi) + 2.0 * fabs(glo) + 1.0;
     }
+    const int m4 = (m + 3) & ~3;
     __syncthreads();
     if (i < 64) {
       const int h = i >> 5, j = i & 31;
@@ -491,28 +592,42 @@ __global__ void __launch_bounds__(64 * ((MP + 63) / 64))
       double l = glo, u = ghi;
       for (int it = 0; it < 80; ++it) {
         const double x = l + (u - l) * ((double)(j + 1) * (1.0 / 33.0));
+        /* d and e^2 are padded to a multiple of 4 with decoupled entries above the
+         * spectrum, so the unrolled groups need no tail */
+        double pm = 1.0, pc = 1.0;
         int cnt = 0;
-        double q = s_d[0] - x;
-        if (fabs(q) < pivmin) q = -pivmin;
-        cnt += q < 0.0;
-        for (int k = 1; k < m; ++k) {
-          q = (s_d[k] - x) - s_e2[k - 1] / q;
-          if (fabs(q) < pivmin) q = -pivmin;
-          cnt += q < 0.0;
+        for (int k = 0; k < m4; k += 4) {
+          const double2 d01 = *reinterpret_cast<const double2 *>(s_d + k);
+          const double2 d23 = *reinterpret_cast<const double2 *>(s_d + k + 2);
+          const double2 e01 = *reinterpret_cast<const double2 *>(s_e2 + k);
+          const double2 e23 = *reinterpret_cast<const double2 *>(s_e2 + k + 2);
+          const double dk[4] = {d01.x, d01.y, d23.x, d23.y};
+          const double ek[4] = {e01.x, e01.y, e23.x, e23.y}; /* e_{k-1}^2, s_e2[0] = 0 */
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            double pn = fma(dk[u] - x, pc, -(ek[u] * pm));
+            /* an exactly zero minor takes the sign opposite to its predecessor */
+            pn = (pn == 0.0) ? -pc * DBL_MIN : pn;
+            cnt += (int)((__double2hiint(pn) ^ __double2hiint(pc)) < 0);
+            pm = pc;
+            pc = pn;
+          }
+          const int ex = __builtin_amdgcn_frexp_exp(fmax(fabs(pm), fabs(pc)));
+          pm = __builtin_amdgcn_ldexp(pm, -ex);
+          pc = __builtin_amdgcn_ldexp(pc, -ex);
         }
         double nl = cnt <= target ? x : l;
         double nu = cnt <= target ? u : x;
+        /* half-wave max / min: xor butterflies inside each 32-lane half */
 #pragma unroll
         for (int o = 16; o >= 1; o >>= 1) {
           nl = fmax(nl, __shfl_xor(nl, o));
           nu = fmin(nu, __shfl_xor(nu, o));
         }
-        nl = __shfl(nl, i & 32);
-        nu = __shfl(nu, i & 32);
         const bool same = (nl == l && nu == u);
         l = nl;
         u = nu;
-        const bool conv = same || (u - l) <= 2.0 * DBL_EPSILON * fmax(fabs(l), fabs(u)) + pivmin;
+        const bool conv = same || (u - l) <= 2.0 * DBL_EPSILON * fmax(fabs(l), fabs(u)) + DBL_MIN;
         if (__all(conv)) break;
       }
       if (j == 0) {
@@ -522,93 +637,114 @@ __global__ void __launch_bounds__(64 * ((MP + 63) / 64))
     }
     __syncthreads();
 
-    /* ---- eigenvectors of T by inverse iteration (partial-pivot LU of T - lam I),
-     * lane 0 for the largest, lane 1 for the second */
+    CSS_PROF(3);
+    /* ---- eigenvectors of T: two steps of inverse iteration with a partial-pivot
+     * LU of T - lam I (lane 0: largest, lane 1: second).  The serial chains carry
+     * their running values in registers; LDS holds only read-once factors. */
     if (i < 2) {
       const double sig = s_lam[i];
       const double tiny = DBL_EPSILON * fmax(fmax(fabs(glo), fabs(ghi)), DBL_MIN);
       double *U0 = s_lu[i][0], *U1 = s_lu[i][1], *U2 = s_lu[i][2];
-      double *y = s_y[i];
       double *ml = s_x + i * MP; /* elimination multipliers; s_x is free until X is formed */
       uint8_t *pv = s_piv[i];
       double c0 = s_d[0] - sig, c1 = m > 1 ? s_e[0] : 0.0;
       for (int k = 0; k < m - 1; ++k) {
         const double n0 = s_e[k], n1 = s_d[k + 1] - sig, n2 = (k + 2 < m) ? s_e[k + 1] : 0.0;
-        if (fabs(c0) >= fabs(n0)) {
-          const double t = (c0 != 0.0) ? n0 / c0 : 0.0;
-          U0[k] = c0;
-          U1[k] = c1;
-          U2[k] = 0.0;
-          ml[k] = t;
-          pv[k] = 0;
-          c0 = n1 - t * c1;
-          c1 = n2;
-        } else {
-          const double t = c0 / n0;
-          U0[k] = n0;
-          U1[k] = n1;
-          U2[k] = n2;
-          ml[k] = t;
-          pv[k] = 1;
-          c0 = c1 - t * n1;
-          c1 = -t * n2;
-        }
+        const bool sw = fabs(c0) < fabs(n0);
+        const double pvt = sw ? n0 : c0, oth = sw ? c0 : n0;
+        const double t = (pvt != 0.0) ? oth * fast_rcp(pvt) : 0.0;
+        U0[k] = pvt;
+        U1[k] = sw ? n1 : c1;
+        U2[k] = sw ? n2 : 0.0;
+        ml[k] = t;
+        pv[k] = sw;
+        const double nc0 = sw ? fma(-t, n1, c1) : fma(-t, c1, n1);
+        c1 = sw ? -t * n2 : n2;
+        c0 = nc0;
       }
       U0[m - 1] = c0;
-      for (int k = 0; k < m; ++k)
-        if (U0[k] == 0.0) U0[k] = tiny;
       /* start vector: deterministic, not orthogonal to anything in practice */
       for (int k = 0; k < m; ++k) {
         const double f = (double)((k * 40503u + 977u * (unsigned)(i + 1)) & 1023u) / 1024.0;
-        y[k] = (i == 0 ? 1.0 : ((k & 1) ? -1.0 : 1.0)) * (0.5 + f);
-      }
-      for (int itn = 0; itn < 3; ++itn) {
-        for (int k = 0; k < m - 1; ++k) {
-          if (pv[k]) {
-            const double t = y[k];
-            y[k] = y[k + 1];
-            y[k + 1] = t;
-          }
-          y[k + 1] -= ml[k] * y[k];
-        }
-        y[m - 1] = y[m - 1] / U0[m - 1];
-        if (m > 1) y[m - 2] = (y[m - 2] - U1[m - 2] * y[m - 1]) / U0[m - 2];
-        for (int k = m - 3; k >= 0; --k) y[k] = (y[k] - U1[k] * y[k + 1] - U2[k] * y[k + 2]) / U0[k];
-        double mx = 0;
-        for (int k = 0; k < m; ++k) mx = fmax(mx, fabs(y[k]));
-        const double inv = mx > 0 ? 1.0 / mx : 1.0;
-        double nrm = 0;
-        for (int k = 0; k < m; ++k) {
-          y[k] *= inv;
-          nrm += y[k] * y[k];
-        }
-        const double r = 1.0 / sqrt(nrm);
-        for (int k = 0; k < m; ++k) y[k] *= r;
+        s_y[i][k] = (i == 0 ? 1.0 : ((k & 1) ? -1.0 : 1.0)) * (0.5 + f);
       }
     }
     __syncthreads();
+    if (row) {
+      /* reciprocal pivots, in parallel (zero pivots -> tiny) */
+      const double tiny = DBL_EPSILON * fmax(fmax(fabs(glo), fabs(ghi)), DBL_MIN);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const double u0 = s_lu[h][0][i];
+        s_lu[h][0][i] = fast_rcp(u0 == 0.0 ? tiny : u0);
+      }
+    }
+    double y1 = 0.0, y2 = 0.0;
+    for (int itn = 0; itn < 2; ++itn) {
+      __syncthreads();
+      if (i < 2) {
+        double *y = s_y[i];
+        const double *R0 = s_lu[i][0], *U1 = s_lu[i][1], *U2 = s_lu[i][2], *ml = s_x + i * MP;
+        const uint8_t *pv = s_piv[i];
+        double yk = y[0];
+        for (int k = 0; k < m - 1; ++k) {
+          double yn = y[k + 1];
+          if (pv[k]) {
+            const double t = yk;
+            yk = yn;
+            yn = t;
+          }
+          y[k] = yk;
+          yk = fma(-ml[k], yk, yn);
+        }
+        double z1 = yk * R0[m - 1], z2 = 0.0;
+        y[m - 1] = z1;
+        for (int k = m - 2; k >= 0; --k) {
+          const double z0 = (y[k] - U1[k] * z1 - U2[k] * z2) * R0[k];
+          y[k] = z0;
+          z2 = z1;
+          z1 = z0;
+        }
+      }
+      __syncthreads();
+      y1 = row ? s_y[0][ii] : 0.0;
+      y2 = row ? s_y[1][ii] : 0.0;
+      double n1 = y1 * y1, n2 = y2 * y2;
+      block_sum2<NW>(n1, n2, s_red);
+      y1 *= 1.0 / sqrt(n1);
+      y2 *= 1.0 / sqrt(n2);
+      if (itn == 0 && row) {
+        s_y[0][i] = y1;
+        s_y[1][i] = y2;
+      }
+    }
     /* orthogonalise the second vector against the first (close eigenvalues) */
-    double y1 = row ? s_y[0][ii] : 0.0, y2 = row ? s_y[1][ii] : 0.0;
     {
-      const double dt = block_sum<NW>(y1 * y2, s_red);
-      y2 -= dt * y1;
-      const double n2 = block_sum<NW>(y2 * y2, s_red);
+      double dt = y1 * y2, zero = 0.0;
+      block_sum2<NW>(dt, zero, s_red);
+      y2 = fma(-dt, y1, y2);
+      double n2 = y2 * y2;
+      zero = 0.0;
+      block_sum2<NW>(n2, zero, s_red);
       y2 *= 1.0 / sqrt(n2);
     }
 
+    CSS_PROF(4);
     /* ---- back-transformation y <- H_0 H_1 ... H_{m-3} y */
 #pragma unroll
     for (int k = MP - 3; k >= 0; --k) {
       if (k <= m - 3) {
         const double vk = row ? A[k] : 0.0;
         const double t = s_tau[k];
-        const double d1 = block_sum<NW>(vk * y1, s_red);
-        const double d2 = block_sum<NW>(vk * y2, s_red);
-        y1 -= (t * d1) * vk;
-        y2 -= (t * d2) * vk;
+        double d1 = vk * y1, d2 = vk * y2;
+        block_sum2<NW>(d1, d2, s_red);
+        y1 = fma(-(t * d1), vk, y1);
+        y2 = fma(-(t * d2), vk, y2);
+        asm volatile("" ::: "memory"); /* one s_tau load in flight, not MP */
       }
     }
 
+    CSS_PROF(5);
     /* ---- X = Q sqrt(L) (css.c:545-556), then calc_dist + css on identity groups */
     {
       const double L1 = sqrt(s_lam[0]), L2 = sqrt(s_lam[1]);
@@ -620,6 +756,7 @@ __global__ void __launch_bounds__(64 * ((MP + 63) / 64))
       __syncthreads();
     }
     const double score = css_score<NW>(s_tr, a, b, [&](int p, int q) { return xdist(s_x, p, q); }, s_red);
+    CSS_PROF(6);
     if (score == -1.0) continue; /* the reference's "discarded" marker (css.c:127) */
     if (i == 0) {
       scores[d.w_out + wl] = score;
@@ -644,7 +781,7 @@ __global__ void __launch_bounds__(64 * ((MP + 63) / 64))
   __shared__ double s_x[2 * MP];
   __shared__ int s_tr[MP];
   __shared__ gd_randint s_rd[MP + 1];
-  __shared__ double s_red[NW];
+  __shared__ double s_red[2 * NW];
   const int i = threadIdx.x;
   for (int n = i; n <= MP; n += NT) s_rd[n] = gd_randint_make(n < 1 ? 1u : (uint32_t)n);
 
@@ -709,14 +846,14 @@ static int launch_tier(const gd_chrom_dev *d_ch, int nchrom, const gd_css_planes
                        double *xbuf, uint8_t *status, unsigned *flags, hipStream_t s) {
   constexpr int NT = 64 * ((MP + 63) / 64);
   const int want_x = (runs > 0 && treshold > 0) ? 1 : 0;
-  const unsigned gx = (unsigned)std::min<int64_t>(wtotal, 256 * 32);
+  const unsigned gx = (unsigned)wtotal;
   const char *fl = getenv("GD_CSS_FORCE_LITERAL"); /* diagnostics: per-SNP predicate for every window */
   const int force_literal = (fl && fl[0] == '1') ? 1 : 0;
   hipLaunchKernelGGL(k_css_mds<MP>, dim3(gx), dim3(NT), 0, s, d_ch, nchrom, d_pl, planes, lo_a, hi_a, lo_b, avals,
                      bvals, wtotal, want_x, force_literal, scores, p, xbuf, status, flags);
   if (hipGetLastError() != hipSuccess) return GD_ERR_HIP;
   if (want_x) {
-    hipLaunchKernelGGL(k_css_perm<MP>, dim3(gx), dim3(NT), 0, s, d_ch, nchrom, xbuf, status, wtotal,
+    hipLaunchKernelGGL(k_css_perm<MP>, dim3((unsigned)std::min<int64_t>(wtotal, 256 * 32)), dim3(NT), 0, s, d_ch, nchrom, xbuf, status, wtotal,
                        treshold, runs, p);
     if (hipGetLastError() != hipSuccess) return GD_ERR_HIP;
   }
@@ -734,6 +871,22 @@ int gd_css_launch(int mp, const gd_chrom_dev *d_ch, int nchrom, const gd_css_pla
                        planes);
     if (hipGetLastError() != hipSuccess) return GD_ERR_HIP;
   }
+#ifdef GD_CSS_PROFILE
+  {
+    static const unsigned long long z[8] = {0};
+    (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_css_prof), z, sizeof z, 0, hipMemcpyHostToDevice, s);
+  }
+  struct Dump {
+    hipStream_t s;
+    ~Dump() {
+      unsigned long long h[8];
+      (void)hipStreamSynchronize(s);
+      (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(g_css_prof), sizeof h);
+      fprintf(stderr, "css-prof cycles: D %llu fill+center %llu tridiag %llu bisect %llu invit %llu back %llu score %llu\n",
+              h[0], h[1], h[2], h[3], h[4], h[5], h[6]);
+    }
+  } dump{s};
+#endif
   switch (mp) {
     case 24:
       return launch_tier<24>(d_ch, nchrom, d_pl, planes, lo_a, hi_a, lo_b, avals, bvals, wtotal, treshold, runs,
