@@ -11,9 +11,18 @@ the device before timing; weak scaling: every rank scans its own 20 chromosomes
 Prints ONE JSON line (rank 0).  `roofline` prices the whole scan's algorithmic
 HBM bytes B = 12*(alen+blen) + 16*W (f64 value + i32 position per
 genotype, two f64 outputs per window) against its kernel time, and also lists each
-stage's kernel time.  `cpu_baseline` times the reference's own Pthreads threadcompute()
-(oracle/_ref, compiled from the reference sources) on a bounded sample of the same
-workload, or the oracle port when that binary is absent.
+stage's kernel time.  `traffic` is the measured HBM bytes per scan from the committed
+rocprofv3 PMC summary (profiles/r01_fet_traffic.json, FETCH_SIZE doubled per the
+gfx950 correction + WRITE_SIZE), or null when absent.  `cpu_baseline` times the
+reference's own Pthreads threadcompute() (oracle/_ref, compiled from the reference
+sources) on a bounded sample of the same workload, or the oracle port when that
+binary is absent.
+
+A second object, `css`, measures the CSS scan (BASELINE.json configs[2]: 1M windows,
+20+20, classical MDS, runs=0) on the same resident chromosomes, priced against the
+FP64 roofline with SURVEY.md 8(d)'s solver-neutral (4/3) m^3 + 10 m^2 flops per
+window, with the CPU oracle port timed on a sample beside it (the reference CSS
+needs GSL, absent from the image, so no reference binary exists).
 """
 from __future__ import annotations
 
@@ -32,6 +41,8 @@ PKG = ROOT / "fast-parallel-tools-for-genome-wide-analysis-of-genomic-divergence
 sys.path.insert(0, str(PKG))
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, HBM3E spec
+FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 vector spec; ubench: ~31-37 T FMA/s
+TRAFFIC_FILE = ROOT / "profiles" / "r01_fet_traffic.json"
 
 
 def parse():
@@ -48,7 +59,35 @@ def parse():
     ap.add_argument("--perc", type=float, default=0.95)
     ap.add_argument("--cpu-chroms", type=int, default=20, help="chromosomes in the CPU-baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-css", action="store_true", help="skip the CSS leg")
+    ap.add_argument("--css-steps", type=int, default=3)
+    ap.add_argument("--css-cpu-snps", type=int, default=150_000, help="SNPs in the CSS CPU-baseline sample")
     return ap.parse_args()
+
+
+def css_cpu_baseline(args):
+    """The CSS oracle port (1 thread) on a prefix of chromosome 0 of the same workload."""
+    from gdscan import synth
+    orc = ROOT / "oracle" / "_build" / "liboracle.so"
+    DP = np.ctypeslib.ndpointer(np.float64, flags="C")
+    IP = np.ctypeslib.ndpointer(np.int32, flags="C")
+    C = ctypes
+    lib = C.CDLL(str(orc))
+    fn = lib.orc_css_scan
+    fn.argtypes = [DP, DP, IP, IP, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_uint64,
+                   C.c_int, DP, DP]
+    av, bv, ap_, bp, regend = synth.chromosome(0, args.css_cpu_snps, args.asize, args.bsize)
+    n = regend // args.wstep
+    s, p = np.zeros(n), np.zeros(n)
+    t0 = time.perf_counter()
+    fn(av, bv, ap_, bp, regend, args.wsize, args.wstep, len(av), len(bv), 10, 0, 1, 0, s, p)
+    dt = time.perf_counter() - t0
+    from gdscan import fet
+    w = fet.window_count(regend, args.wsize, args.wstep)
+    return {"value": w / dt, "unit": "windows/s", "cores": 1, "kind": "port",
+            "sample": f"chromosome 0 prefix, {args.css_cpu_snps} SNPs ({args.asize}+{args.bsize}), {w} windows "
+                      f"in {dt:.2f} s, 1 thread (cyclic-Jacobi restatement; the reference CSS needs GSL, "
+                      f"absent here)"}
 
 
 def cpu_baseline(args):
@@ -217,14 +256,66 @@ def main():
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
             "traffic": None,
-            "kernel": "whole scan (bounds + per-SNP FET + window bootstrap), HIP events per step",
+            "kernel": "whole scan pipeline (k_popsize, k_bounds, k_snp_fet, k_fet_window_fast; k_fet_lut_* "
+                      "when the score table is cold), HIP events on the scan's streams per step",
             "alg_bytes_per_step": alg_bytes,
             "stage_ms": {"hbm_passes_done": stage[0], "fast_windows_done": stage[1],
                          "general_path": stage[2], "scan_total": stage[3]},
         },
     }
+    if TRAFFIC_FILE.exists():
+        tr = json.loads(TRAFFIC_FILE.read_text())
+        if tr.get("config") == [nch, nsnp, a, b]:
+            out["roofline"]["traffic"] = tr["bytes_per_scan"]
+            out["roofline"]["traffic_source"] = f"{TRAFFIC_FILE.relative_to(ROOT)} ({tr['method']})"
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(args)
+
+    if not args.no_css:
+        pv = torch.zeros_like(scores)
+
+        def css_step():
+            check(lib.gd_css_scan_device(ctx, chroms, nch, avals.data_ptr(), bvals.data_ptr(), apos.data_ptr(),
+                                         bpos.data_ptr(), args.wsize, args.wstep, 10, 0, _lib.GD_WINDOWS_THREADED,
+                                         scores.data_ptr(), pv.data_ptr(), stream))
+
+        css_step()
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        kms = 0.0
+        for _ in range(args.css_steps):
+            css_step()
+            kms += _lib.last_stage_ms()[1]  # the CSS window kernel (bit planes -> scores)
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        css_elapsed = time.perf_counter() - t0
+        if dist:
+            t = torch.tensor([css_elapsed], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            css_elapsed = float(t.item())
+        kms /= args.css_steps
+        m = a + b
+        flops = (4.0 / 3.0 * m ** 3 + 10.0 * m * m) * windows
+        ach = flops / (kms * 1e-3) / 1e12
+        out["css"] = {
+            "metric": "CSS genomic windows/sec (classical MDS, runs=0; per-GPU batch)",
+            "value": windows * world * args.css_steps / css_elapsed,
+            "unit": "windows/s",
+            "ms_per_step": css_elapsed * 1e3 / args.css_steps,
+            "steps": args.css_steps,
+            "config": {"workload": f"CSS, configs[2] shape: {nch} chromosomes x {nsnp} SNPs per GPU, {a}+{b} "
+                                   f"individuals, wsize {args.wsize}, wstep {args.wstep}, mcR=0",
+                       "windows_per_gpu": windows},
+            "roofline": {"bound": "fp64-valu", "achieved": ach, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                         "frac": ach / FP64_PEAK_TFLOPS, "traffic": None,
+                         "kernel": "k_css_pack + k_css_mds (HIP events)", "kernel_ms": kms,
+                         "alg_flops_per_window": flops / windows},
+        }
+        if rank == 0 and world == 1 and not args.no_cpu:
+            out["css"]["cpu_baseline"] = css_cpu_baseline(args)
     lib.gd_ctx_destroy(ctx)
     if rank == 0:
         print(json.dumps(out), flush=True)

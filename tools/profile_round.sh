@@ -1,0 +1,20 @@
+#!/bin/bash
+# One GPU-box profiling pass for a round: bench line, kernel trace + stats, and the
+# HBM PMC counters (FETCH_SIZE and WRITE_SIZE in separate passes).  Every GPU step
+# has its own time limit and the steps are chained with &&.
+# usage: tools/profile_round.sh r01
+set -o pipefail
+R=${1:-r01}
+O=gpurun_out/$R
+mkdir -p $O
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
+timeout -k 10 420 python bench.py > $O/bench.json 2> $O/bench.err &&
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/ktrace -o run --output-format csv -- \
+    python3 bench.py --steps 5 --warmup 1 --no-cpu > $O/ktrace_bench.json 2> $O/ktrace.err &&
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $O/pmc_fetch -o run --output-format csv -- \
+    python3 bench.py --steps 2 --warmup 1 --no-cpu --no-css > $O/pmc_fetch.json 2> $O/pmc_fetch.err &&
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d $O/pmc_write -o run --output-format csv -- \
+    python3 bench.py --steps 2 --warmup 1 --no-cpu --no-css > $O/pmc_write.json 2> $O/pmc_write.err &&
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $O/pmc_css_fetch -o run --output-format csv -- \
+    python3 bench.py --steps 1 --warmup 0 --no-cpu --css-steps 1 > $O/pmc_css.json 2> $O/pmc_css.err
+echo "profile_round exit $?"
