@@ -224,6 +224,21 @@ def main():
         elapsed = float(t.item())
     stage /= args.steps
     ms_per_step = elapsed * 1e3 / args.steps
+    gather_ms = None
+    if dist:
+        # the one collective of the path: all ranks' (score, stddev) tracks gathered in
+        # genome order; measured once, outside the timed steps
+        from gdscan.shard import gather_tracks
+        wt = torch.zeros(world * nch, dtype=torch.int64, device=dev)
+        wt[rank * nch:(rank + 1) * nch] = torch.tensor([chroms[c].regend // args.wstep for c in range(nch)])
+        dist.all_reduce(wt)  # every rank learns every chromosome's window count
+        shards = [list(range(r * nch, (r + 1) * nch)) for r in range(world)]
+        local = torch.stack([scores, stddev], 1)
+        torch.cuda.synchronize()
+        g0 = time.perf_counter()
+        gather_tracks(local, shards, wt.tolist())
+        torch.cuda.synchronize()
+        gather_ms = (time.perf_counter() - g0) * 1e3
     total_windows = windows * world
     value = total_windows * args.steps / elapsed
 
@@ -248,6 +263,7 @@ def main():
                         "wsize 2500, wstep 500, perc 0.95, 100 bootstrap replicates",
             "chromosomes_per_gpu": nch, "snps_per_gpu": nch * nsnp, "windows_per_gpu": windows,
             "asize": a, "bsize": b, "parallelism": f"window-sharded x{world} (whole chromosomes per rank)",
+            "track_gather_ms": gather_ms,
         },
         "roofline": {
             "bound": "hbm",

@@ -1,0 +1,56 @@
+"""Multi-GPU sharding of a genome-wide scan.
+
+Windows depend only on the SNPs they cover, so a genome shards by whole
+chromosomes: each rank (one process per GPU) scans its own chromosomes with no
+data-path exchange.  The only collective is the optional gather of the finished
+per-window tracks (score, stddev|p: 16 B per window) to one rank, as equal-padded
+slices of one all-gather (RCCL over xGMI on GPUs, gloo in the CPU tests).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+
+def plan_shards(snp_counts, world):
+    """Assign chromosomes to ranks, balancing SNPs (longest-processing-time greedy).
+
+    Deterministic: ties go to the lowest rank.  Returns one sorted list of
+    chromosome indices per rank."""
+    order = sorted(range(len(snp_counts)), key=lambda c: (-int(snp_counts[c]), c))
+    load = [0] * world
+    out = [[] for _ in range(world)]
+    for c in order:
+        r = min(range(world), key=lambda k: (load[k], k))
+        out[r].append(c)
+        load[r] += int(snp_counts[c])
+    return [sorted(x) for x in out]
+
+
+def gather_tracks(local, shards, windows_per_chrom, group=None):
+    """All-gather every rank's concatenated per-window track into genome order.
+
+    local: tensor [n_local_windows, k] -- this rank's chromosomes, in shard order.
+    shards: plan_shards() output; windows_per_chrom: windows of every chromosome.
+    Returns the [total_windows, k] track on every rank (CPU or device tensor,
+    matching `local`)."""
+    import torch
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group)
+    counts = [sum(int(windows_per_chrom[c]) for c in s) for s in shards]
+    width = local.shape[1] if local.dim() == 2 else 1
+    pad = max(counts) if counts else 0
+    buf = torch.zeros((pad, width), dtype=local.dtype, device=local.device)
+    buf[: local.shape[0]] = local.reshape(-1, width)
+    out = torch.empty((world * pad, width), dtype=local.dtype, device=local.device)
+    dist.all_gather_into_tensor(out, buf, group=group)
+    offs = np.concatenate([[0], np.cumsum([int(w) for w in windows_per_chrom])])
+    total = int(offs[-1])
+    track = torch.empty((total, width), dtype=local.dtype, device=local.device)
+    for r, s in enumerate(shards):
+        pos = 0
+        for c in s:
+            n = int(windows_per_chrom[c])
+            track[offs[c]:offs[c] + n] = out[r * pad + pos: r * pad + pos + n]
+            pos += n
+    return track

@@ -1,0 +1,80 @@
+"""CPU: chromosome sharding and the track gather over torch.distributed (gloo,
+world_size 2).  Each rank scans its shard with the CPU oracle standing in for the
+device scan; the gathered track must equal the single-process genome scan."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+
+def test_plan_shards_balances_and_covers():
+    from gdscan.shard import plan_shards
+    counts = [500, 480, 300, 300, 120, 90, 60, 10]
+    for world in (1, 2, 3, 8):
+        shards = plan_shards(counts, world)
+        assert sorted(c for s in shards for c in s) == list(range(len(counts)))
+        loads = [sum(counts[c] for c in s) for s in shards]
+        assert max(loads) - min(loads) <= max(counts)
+    assert plan_shards(counts, 2) == plan_shards(counts, 2)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, q):
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parent
+    sys.path.insert(0, str(root))
+    import ctypes
+    import torch
+    import torch.distributed as dist
+    from conftest import ORACLE_LIB, DP, IP, oracle_fet_scan
+    from gdscan import synth
+    from gdscan.shard import gather_tracks, plan_shards
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    orc = ctypes.CDLL(str(ORACLE_LIB))
+    C = ctypes
+    orc.orc_fet_scan.argtypes = [DP, DP, IP, IP, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_double,
+                                 C.c_uint64, C.c_int, DP, DP]
+    sizes = [9000, 4000, 7000, 3000, 6000]
+    chroms = [synth.chromosome(40 + c, n, 6, 6) for c, n in enumerate(sizes)]
+    wins = [x[4] // 500 for x in chroms]
+    shards = plan_shards(sizes, world)
+    parts = []
+    for c in shards[rank]:
+        av, bv, ap, bp, regend = chroms[c]
+        s, d = oracle_fet_scan(orc, av, bv, ap, bp, regend, seed=100 + c)
+        parts.append(np.stack([s, d], 1))
+    local = torch.from_numpy(np.concatenate(parts) if parts else np.zeros((0, 2)))
+    track = gather_tracks(local, shards, wins).numpy()
+    if rank == 0:
+        ref = []
+        for c, (av, bv, ap, bp, regend) in enumerate(chroms):
+            s, d = oracle_fet_scan(orc, av, bv, ap, bp, regend, seed=100 + c)
+            ref.append(np.stack([s, d], 1))
+        q.put(bool(np.array_equal(track, np.concatenate(ref))))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gather_tracks_gloo_world2(oracle):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=300)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    assert q.get(timeout=10) is True
