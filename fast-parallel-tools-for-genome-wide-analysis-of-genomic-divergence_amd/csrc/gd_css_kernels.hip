@@ -54,6 +54,11 @@ __device__ unsigned long long g_css_prof[8];
 #define CSS_PROF(ph)
 #endif
 
+/* waves per SIMD the register allocator must reach for k_css_mds<MP>: the kernel is
+ * latency-bound, so occupancy beats the few cold spills it costs (MP=40: 4 waves,
+ * 12 VGPRs spilled, 9 % faster than the unconstrained 3 waves) */
+#define CSS_MDS_WAVES(MP) ((MP) <= 24 ? 5 : (MP) <= 40 ? 4 : (MP) <= 64 ? 2 : 1)
+
 namespace {
 
 /* bits [bit, bit + 64) of a bit plane (planes carry 3 words of zero padding) */
@@ -283,7 +288,7 @@ __global__ void __launch_bounds__(256) k_css_pack(const gd_chrom_dev *ch, const 
 /* per-window classical MDS + CSS                                              */
 /* ------------------------------------------------------------------------ */
 template <int MP>
-__global__ void __launch_bounds__(64 * ((MP + 63) / 64))
+__global__ void __launch_bounds__(64 * ((MP + 63) / 64), CSS_MDS_WAVES(MP))
     k_css_mds(const gd_chrom_dev *ch, int nchrom, const gd_css_planes *pl, const uint32_t *planes,
               const int32_t *lo_a_, const int32_t *hi_a_, const int32_t *lo_b_, const double *avals,
               const double *bvals, int64_t wtotal, int want_x, int force_literal, double *scores, double *pvals,
