@@ -77,7 +77,8 @@ struct gd_ctx {
   int device = 0;
   std::mutex mu;
   hipStream_t stream = nullptr;  /* used by the host entry points */
-  hipStream_t stream2 = nullptr; /* second stream of the pipelined scans */
+  hipStream_t stream2 = nullptr;    /* window kernels of the pipelined scans (lowest priority) */
+  hipStream_t stream_mem = nullptr; /* HBM-bound passes of the pipelined scans (highest priority) */
   hipEvent_t gev[GD_MAX_GROUPS] = {};
   char *ws = nullptr;
   size_t ws_cap = 0;
@@ -98,7 +99,13 @@ static int ctx_init(gd_ctx *c, int device) {
   c->device = device;
   HIP_TRY(hipSetDevice(device));
   HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-  HIP_TRY(hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking));
+  {
+    /* the memory passes feed the window kernels: give them the CUs first */
+    int least = 0, greatest = 0;
+    HIP_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
+    HIP_TRY(hipStreamCreateWithPriority(&c->stream2, hipStreamNonBlocking, least));
+    HIP_TRY(hipStreamCreateWithPriority(&c->stream_mem, hipStreamNonBlocking, greatest));
+  }
   for (auto &e : c->gev) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   HIP_TRY(hipMalloc(&c->binom, sizeof(uint64_t) * GD_BINOM_ENTRIES));
   hipLaunchKernelGGL(k_binom_table, dim3((GD_BINOM_ENTRIES + 255) / 256), dim3(256), 0, c->stream, c->binom);
@@ -136,6 +143,7 @@ extern "C" void gd_ctx_destroy(gd_ctx *c) {
   for (auto &e : c->gev)
     if (e) (void)hipEventDestroy(e);
   if (c->stream2) (void)hipStreamDestroy(c->stream2);
+  if (c->stream_mem) (void)hipStreamDestroy(c->stream_mem);
   if (c->h_flags) (void)hipHostFree(c->h_flags);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
@@ -299,17 +307,21 @@ static int fet_scan_locked(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, cons
   HIP_TRY(hipMemcpyAsync(d_blk, blk_off.data(), sizeof(int32_t) * (nchrom + 1), hipMemcpyHostToDevice, s));
   HIP_TRY(hipMemsetAsync(flags, 0, 16 * sizeof(unsigned), s));
   HIP_TRY(hipEventRecord(ctx->ev[0], s));
-  hipLaunchKernelGGL(k_popsize, dim3(nchrom), dim3(64), 0, s, d_ch, apos, bpos, flags);
+  /* Pipeline over chromosome groups on the context's two streams: the HBM-bound
+   * passes (bounds + per-SNP FET) run on the high-priority stream and feed the
+   * VALU-bound bootstrap of each group on the low-priority stream as soon as the
+   * group's rows are scored.  The caller's stream `s` orders the scan against its
+   * other work. */
+  hipStream_t sm = ctx->stream_mem, s2 = ctx->stream2;
+  HIP_TRY(hipStreamWaitEvent(sm, ctx->ev[0], 0));
+  hipLaunchKernelGGL(k_popsize, dim3(nchrom), dim3(64), 0, sm, d_ch, apos, bpos, flags);
   bool force_general = false;
-  if ((st = gd_fet_window_prepare(pl.wtotal, list, list_count, s, &force_general))) return st;
+  if ((st = gd_fet_window_prepare(pl.wtotal, list, list_count, sm, &force_general))) return st;
   /* score table for chromosome 0's population sizes (no-op when cached) */
-  hipLaunchKernelGGL(k_fet_lut_build, dim3(512), dim3(256), 0, s, d_ch, ctx->binom, ctx->lut_hdr, ctx->lut,
+  hipLaunchKernelGGL(k_fet_lut_build, dim3(512), dim3(256), 0, sm, d_ch, ctx->binom, ctx->lut_hdr, ctx->lut,
                      (int64_t)GD_LUT_CAP);
-  hipLaunchKernelGGL(k_fet_lut_publish, dim3(1), dim3(1), 0, s, d_ch, ctx->lut_hdr, (int64_t)GD_LUT_CAP);
+  hipLaunchKernelGGL(k_fet_lut_publish, dim3(1), dim3(1), 0, sm, d_ch, ctx->lut_hdr, (int64_t)GD_LUT_CAP);
 
-  /* Pipeline over chromosome groups: the HBM-bound passes (bounds + per-SNP FET)
-   * of group g+1 run on stream s while the VALU-bound bootstrap of group g runs on
-   * the context's second stream. */
   int G = std::min(nchrom, GD_MAX_GROUPS);
   if (const char *eg = getenv("GD_GROUPS")) G = std::max(1, std::min(G, atoi(eg))); /* diagnostics */
   std::vector<int> cuts(G + 1);
@@ -323,17 +335,15 @@ static int fet_scan_locked(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, cons
       mx = std::max<int64_t>(mx, std::max(pl.h[c].alen, pl.h[c].blen) + 1);
     }
     const unsigned gxb = (unsigned)std::min<int64_t>((mx + 4095) / 4096, std::max(1, 8192 / nc));
-    hipLaunchKernelGGL(k_bounds, dim3(gxb, nc, 2), dim3(256), 0, s, d_ch + c0, apos, bpos, wsize, wstep, lo_a,
+    hipLaunchKernelGGL(k_bounds, dim3(gxb, nc, 2), dim3(256), 0, sm, d_ch + c0, apos, bpos, wsize, wstep, lo_a,
                        hi_a, lo_b, flags);
     const unsigned gxs = (unsigned)std::min<int64_t>((amax + 255) / 256, std::max(1, 8192 / nc));
-    hipLaunchKernelGGL(k_snp_fet, dim3(gxs, nc), dim3(256), 0, s, d_ch + c0, avals, bvals, ctx->binom,
+    hipLaunchKernelGGL(k_snp_fet, dim3(gxs, nc), dim3(256), 0, sm, d_ch + c0, avals, bvals, ctx->binom,
                        ctx->lut_hdr, ctx->lut, snp);
     HIP_TRY(hipGetLastError());
-    HIP_TRY(hipEventRecord(ctx->gev[g], s));
+    HIP_TRY(hipEventRecord(ctx->gev[g], sm));
   }
-  HIP_TRY(hipEventRecord(ctx->ev[1], s));
-  hipStream_t s2 = ctx->stream2;
-  HIP_TRY(hipStreamWaitEvent(s2, ctx->ev[0], 0));
+  HIP_TRY(hipEventRecord(ctx->ev[1], sm));
   for (int g = 0; g < G && !force_general; ++g) {
     const int c0 = cuts[g], c1 = cuts[g + 1];
     HIP_TRY(hipStreamWaitEvent(s2, ctx->gev[g], 0));
@@ -342,6 +352,7 @@ static int fet_scan_locked(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, cons
     if (st) return fail(st, "fast window kernel launch failed");
   }
   HIP_TRY(hipEventRecord(ctx->ev[2], s2));
+  HIP_TRY(hipStreamWaitEvent(s, ctx->ev[1], 0));
   HIP_TRY(hipStreamWaitEvent(s, ctx->ev[2], 0));
   {
     /* windows the fast path declined: literal one-workgroup-per-window path */

@@ -29,6 +29,7 @@
  */
 #include <hip/hip_runtime.h>
 
+#include <cstdio>
 #include <cstdlib>
 
 #include "../../include/gdscan.h"
@@ -40,11 +41,28 @@
 #define FW_RPT 13    /* replicates per lane (8*13 >= 100; the last lane runs 9) */
 #define FW_KTOP 24   /* ranked top scores kept per window (P(needing more) < 1e-9 per replicate) */
 #define FW_NFAST 256 /* largest window handled here */
-#define FW_SPAN 2048 /* staged SNP rows per workgroup */
+#define FW_SPAN 1024 /* staged SNP rows per workgroup (32 windows need ~400 at 50 SNPs/window) */
 #define FW_MAXREJ 8  /* rejected draws tracked per window before giving up */
 
 #define FW_BAD_GENERAL 1 /* hand the window to the literal general path */
 #define FW_BAD_REJECT 2  /* a draw was rejected: redo with corrected offsets (B') */
+
+#ifdef GD_FET_PROFILE
+/* diagnostics build only: shader-clock cycles per phase summed over workgroups (thread 0) */
+__device__ unsigned long long g_fet_prof[8];
+#define FW_PROF_INIT uint64_t prof_t = __builtin_readcyclecounter()
+#define FW_PROF(ph)                                                   \
+  do {                                                                \
+    if (threadIdx.x == 0) {                                           \
+      const uint64_t t_ = __builtin_readcyclecounter();              \
+      atomicAdd(&g_fet_prof[ph], (unsigned long long)(t_ - prof_t)); \
+      prof_t = t_;                                                    \
+    }                                                                 \
+  } while (0)
+#else
+#define FW_PROF_INIT
+#define FW_PROF(ph)
+#endif
 
 namespace {
 
@@ -99,14 +117,15 @@ __device__ __forceinline__ int fmod_n(uint32_t r, uint32_t magic, uint32_t shift
     top_insert<MT>(K, fmod_n(yhi >> 1, rd.magic, rd.shift, rd.n));   \
   } while (0)
 
-/* lane's replicates [r0, r1): y already positioned at stream position r0*n.
- * ymax collects the high words; a draw was rejected iff (ymax >> 1) > limit. */
+/* lane's replicates [r0, r1) (r1 - r0 <= FW_RPT) into rep[0 .. r1-r0): y already
+ * positioned at stream position r0*n.  ymax collects the high words; a draw was
+ * rejected iff (ymax >> 1) > limit. */
 template <int MT>
-__device__ __forceinline__ void boot_lane(uint64_t y, int n, const gd_randint &rd, int r0, int r1, int m, int base,
-                                          double delta, const double *top, double *rep, uint32_t &ymax,
+__device__ __forceinline__ void boot_lane(uint64_t y, int n, const gd_randint &rd, int nr, int m, int base,
+                                          double delta, const double *top, double (&rep)[FW_RPT], uint32_t &ymax,
                                           int &worst) {
   uint32_t ylo = (uint32_t)y, yhi = (uint32_t)(y >> 32);
-  for (int r = r0; r < r1; ++r) {
+  for (int k = 0; k < nr; ++k) {
     int K[MT];
 #pragma unroll
     for (int i = 0; i < MT; ++i) K[i] = -1;
@@ -129,16 +148,19 @@ __device__ __forceinline__ void boot_lane(uint64_t y, int n, const gd_randint &r
       if (i == m - 2) b = K[i];
     }
     worst = min(worst, a); /* a = t_{m-1} <= b = t_{m-2}: the lowest index read */
-    rep[r] = gd_perc_mix(delta, top[max(a - base, 0)], top[max(b - base, 0)]);
+    const double val = gd_perc_mix(delta, top[max(a - base, 0)], top[max(b - base, 0)]);
+    /* replicate k into register slot k (a select per slot keeps rep out of scratch) */
+#pragma unroll
+    for (int u = 0; u < FW_RPT; ++u) rep[u] = (u == k) ? val : rep[u];
   }
 }
 
 /* Rare second pass for a window whose stream contains rejected draws
  * (random_int_nrand48 redraws while r > limit, cFisher.c:550-552): every draw
  * loops until accepted, starting from the lane's corrected stream position. */
-__device__ void boot_lane_rejecting(uint64_t y, int n, const gd_randint &rd, int r0, int r1, int m, int base,
-                                    double delta, const double *top, double *rep, int &worst) {
-  for (int r = r0; r < r1; ++r) {
+__device__ void boot_lane_rejecting(uint64_t y, int n, const gd_randint &rd, int nr, int m, int base,
+                                    double delta, const double *top, double (&rep)[FW_RPT], int &worst) {
+  for (int k = 0; k < nr; ++k) {
     int K[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) K[i] = -1;
@@ -157,23 +179,10 @@ __device__ void boot_lane_rejecting(uint64_t y, int n, const gd_randint &rd, int
       if (i == m - 2) b = K[i];
     }
     worst = min(worst, a);
-    rep[r] = gd_perc_mix(delta, top[max(a - base, 0)], top[max(b - base, 0)]);
+    const double val = gd_perc_mix(delta, top[max(a - base, 0)], top[max(b - base, 0)]);
+#pragma unroll
+    for (int u = 0; u < FW_RPT; ++u) rep[u] = (u == k) ? val : rep[u];
   }
-}
-
-__device__ double std_reverse_lds(const double *a) {
-  double sum = 0;
-#pragma unroll 4
-  for (int i = GD_NREP - 1; i >= 0; --i) sum += a[i];
-  const double mu = sum / GD_NREP;
-  double ss = 0;
-#pragma unroll 4
-  for (int i = GD_NREP - 1; i >= 0; --i) {
-    const double dd = a[i] - mu;
-    ss += dd * dd;
-  }
-  ss /= GD_NREP;
-  return sqrt(ss);
 }
 
 }  // namespace
@@ -200,14 +209,13 @@ __global__ void __launch_bounds__(FW_WPB *FW_TPW)
                       unsigned *slow_count) {
   __shared__ double sh_span[FW_SPAN];
   __shared__ double sh_top[FW_WPB][FW_KTOP];
-  /* the replicate table; before phase B it holds the lanes' locally sorted scores */
-  __shared__ double sh_rep[FW_WPB][GD_NREP];
   __shared__ int64_t sh_row[FW_WPB]; /* snp_score index of the window's first row; -1: not fast */
   __shared__ int sh_n[FW_WPB], sh_key[FW_WPB], sh_bad[FW_WPB], sh_slot[FW_WPB], sh_nrej[FW_WPB];
   __shared__ int sh_rej[FW_WPB][FW_MAXREJ];
   __shared__ unsigned long long sh_lo, sh_hi;
 
   if (*flags & (GD_FLAG_UNSORTED_A | GD_FLAG_UNSORTED_B | GD_FLAG_BAD_SIZE)) return;
+  FW_PROF_INIT;
   const int tid = threadIdx.x;
   /* workgroups never straddle chromosomes: blk_off[c] = first workgroup of chromosome c */
   const int b = blk_base + blockIdx.x;
@@ -279,6 +287,7 @@ __global__ void __launch_bounds__(FW_WPB *FW_TPW)
   for (int i = tid; i < spanlen; i += FW_WPB * FW_TPW) sh_span[i] = snp_score[span0 + i];
   __syncthreads();
 
+  FW_PROF(0);
   const int wl = sh_slot[tid / FW_TPW], q = tid % FW_TPW;
   const int64_t g = g0 + wl;
   const bool fast = sh_row[wl] >= 0;
@@ -318,20 +327,22 @@ __global__ void __launch_bounds__(FW_WPB *FW_TPW)
       FW_CX(2, 4); FW_CX(3, 5);
       FW_CX(1, 2); FW_CX(3, 4); FW_CX(5, 6);
 #undef FW_CX
-      double *mine = &sh_rep[wl][q * 8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) mine[u] = v[u];
-      int h = 0;
+      /* merge: each round the group's largest head is popped by its lowest lane
+       * (the lane's sorted list shifts up; exhausted slots read -inf) */
       const int gbase = (threadIdx.x & 63) & ~7; /* first lane of this group in the wave */
       for (int t = 0; t < ktop; ++t) {
-        const double c = (h < cnt) ? mine[h] : -__builtin_inf();
+        const double c = v[0];
         const double cmax = group8_max(c);
-        /* the lowest lane holding the maximum pops it */
         const uint64_t hit = __ballot(c == cmax);
         const unsigned grp = (unsigned)(hit >> gbase) & 0xFFu;
-        if (q == __builtin_ctz(grp)) ++h;
+        if (q == __builtin_ctz(grp)) {
+#pragma unroll
+          for (int u = 0; u < 7; ++u) v[u] = v[u + 1];
+          v[7] = -__builtin_inf();
+        }
         if (q == 0) sh_top[wl][ktop - 1 - t] = cmax;
       }
+      (void)cnt;
     } else {
       /* 64 < n <= NFAST: rank by counting (ties by position) */
       for (int i = q; i < n; i += FW_TPW) {
@@ -347,6 +358,7 @@ __global__ void __launch_bounds__(FW_WPB *FW_TPW)
   }
   __syncthreads();
 
+  FW_PROF(1);
   /* ---- B. bootstrap replicates: lane q runs replicates [13q, 13q+13) ---- */
   /* order statistics tracked: the largest m among this wave's fast windows */
   int mmax = (fast && sh_bad[wl] == 0) ? m : 0;
@@ -358,21 +370,26 @@ __global__ void __launch_bounds__(FW_WPB *FW_TPW)
   const gd_randint rd = gd_randint_make((uint32_t)(n > 0 ? n : 1));
   uint64_t x0 = 0;
   if (fast) x0 = gd_window_state(d.seed, GD_STREAM_FET, g - d.w_base);
+  double rep[FW_RPT]; /* this lane's replicates r0 .. r1-1 */
+#pragma unroll
+  for (int k = 0; k < FW_RPT; ++k) rep[k] = 0.0;
+  const int nr = r1 - r0;
   if (fast && sh_bad[wl] == 0) {
     const uint64_t x = gd_affine_apply(gd_lcg_jump((uint64_t)r0 * (uint64_t)n), x0);
     uint32_t ymax = 0;
     int worst = n;
     if (mmax <= 4)
-      boot_lane<4>(x << 16, n, rd, r0, r1, m, base, delta, sh_top[wl], sh_rep[wl], ymax, worst);
+      boot_lane<4>(x << 16, n, rd, nr, m, base, delta, sh_top[wl], rep, ymax, worst);
     else if (mmax == 5)
-      boot_lane<5>(x << 16, n, rd, r0, r1, m, base, delta, sh_top[wl], sh_rep[wl], ymax, worst);
+      boot_lane<5>(x << 16, n, rd, nr, m, base, delta, sh_top[wl], rep, ymax, worst);
     else
-      boot_lane<8>(x << 16, n, rd, r0, r1, m, base, delta, sh_top[wl], sh_rep[wl], ymax, worst);
+      boot_lane<8>(x << 16, n, rd, nr, m, base, delta, sh_top[wl], rep, ymax, worst);
     if (worst < base) atomicOr(&sh_bad[wl], FW_BAD_GENERAL);
     if ((ymax >> 1) > rd.limit) atomicOr(&sh_bad[wl], FW_BAD_REJECT);
   }
   __syncthreads();
 
+  FW_PROF(2);
   /* ---- B'. windows whose stream rejected a draw (p ~ n*5000/2^31 per window):
    * lane q locates the rejected positions of its pass-1 range [13qn, 13qn + len),
    * the lanes then restart at the corrected positions P_q = 13qn + #(rejections
@@ -407,30 +424,54 @@ __global__ void __launch_bounds__(FW_WPB *FW_TPW)
       }
       const uint64_t y = gd_affine_apply(gd_lcg_jump((uint64_t)r0 * n + c), x0) << 16;
       int worst = n;
-      boot_lane_rejecting(y, n, rd, r0, r1, m, base, delta, sh_top[wl], sh_rep[wl], worst);
+      boot_lane_rejecting(y, n, rd, nr, m, base, delta, sh_top[wl], rep, worst);
       if (worst < base) atomicOr(&sh_bad[wl], FW_BAD_GENERAL);
     }
   }
   __syncthreads();
 
-  /* ---- C. window score + population std of the 100 replicates (wave 0, one lane per window) ---- */
-  if (tid < FW_WPB && sh_row[tid] >= 0) {
-    const int wn = sh_n[tid];
-    const int wk = wn < FW_KTOP ? wn : FW_KTOP;
-    const int wbase = wn - wk;
-    const int widx = gd_perc_index(wn, perc);
-    const double wdelta = gd_perc_delta(wn, perc, widx);
-    const int64_t wg = g0 + tid;
-    if (sh_bad[tid] & FW_BAD_GENERAL) {
-      slow_list[atomicAdd(slow_count, 1u)] = (int32_t)wg;
+  FW_PROF(3);
+  /* ---- C. window score + population std of the 100 replicates (std, cFisher.c:492-518):
+   * the sums run over i = 99 .. 0 exactly as the reference's loop, as one chain that
+   * walks down the window's 8 lanes (lane q holds replicates 13q ..), handed from
+   * lane to lane with a DPP row shift */
+  const bool live = fast && !(sh_bad[wl] & FW_BAD_GENERAL);
+  double sum = 0.0;
+#pragma unroll
+  for (int step = FW_TPW - 1; step >= 0; --step) {
+    if (live && q == step) {
+#pragma unroll
+      for (int k = FW_RPT - 1; k >= 0; --k)
+        if (k < nr) sum += rep[k];
+    }
+    if (step > 0) sum = dpp_f64<0x101>(sum); /* row_shl:1: lane l takes lane l+1's partial */
+  }
+  const double mu = __shfl(sum, (int)(threadIdx.x & ~7u)) / GD_NREP;
+  double ss = 0.0;
+#pragma unroll
+  for (int step = FW_TPW - 1; step >= 0; --step) {
+    if (live && q == step) {
+#pragma unroll
+      for (int k = FW_RPT - 1; k >= 0; --k)
+        if (k < nr) {
+          const double dd = rep[k] - mu;
+          ss += dd * dd;
+        }
+    }
+    if (step > 0) ss = dpp_f64<0x101>(ss);
+  }
+  if (q == 0 && fast) {
+    if (sh_bad[wl] & FW_BAD_GENERAL) {
+      slow_list[atomicAdd(slow_count, 1u)] = (int32_t)g;
     } else {
-      const int widx1 = (widx + 1 < wn) ? widx + 1 : widx;
-      const double ws = gd_perc_mix(wdelta, sh_top[tid][widx - wbase], sh_top[tid][widx1 - wbase]);
-      const int64_t w = wg - d.w_base;
+      const int widx1 = (idx + 1 < n) ? idx + 1 : idx;
+      const double ws = gd_perc_mix(delta, sh_top[wl][idx - base], sh_top[wl][widx1 - base]);
+      const int64_t w = g - d.w_base;
       scores[d.w_out + w] = ws;
-      stddev[d.w_out + w] = std_reverse_lds(sh_rep[tid]);
+      stddev[d.w_out + w] = sqrt(ss / GD_NREP);
     }
   }
+  FW_PROF(4);
 }
 
 __global__ void k_zero_count(unsigned *count) { *count = 0; }
@@ -464,6 +505,16 @@ int gd_fet_window_fast_launch(const gd_chrom_dev *ch, int nchrom, const int32_t 
                               const double *snp_score, double perc, double *scores, double *stddev,
                               unsigned *flags, int32_t *slow_list, unsigned *slow_count, hipStream_t s) {
   if (blk_count <= 0) return GD_OK;
+#ifdef GD_FET_PROFILE
+  {
+    static int calls = 0;
+    unsigned long long h[8];
+    (void)hipStreamSynchronize(s);
+    (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(g_fet_prof), sizeof h);
+    if (++calls % 8 == 0)
+      fprintf(stderr, "fet-prof cycles: A1 %llu A2 %llu B %llu Bp %llu C %llu\n", h[0], h[1], h[2], h[3], h[4]);
+  }
+#endif
   hipLaunchKernelGGL(k_fet_window_fast, dim3((unsigned)blk_count), dim3(FW_WPB * FW_TPW), 0, s, ch, nchrom, blk_off,
                      blk_begin, lo_a, hi_a, lo_b, snp_score, perc, scores, stddev, flags, slow_list, slow_count);
   return hipGetLastError() == hipSuccess ? GD_OK : GD_ERR_HIP;
