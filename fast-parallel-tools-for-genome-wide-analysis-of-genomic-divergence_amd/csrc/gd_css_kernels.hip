@@ -57,7 +57,7 @@ __device__ unsigned long long g_css_prof[8];
 /* waves per SIMD the register allocator must reach for k_css_mds<MP>: the kernel is
  * latency-bound, so occupancy beats the few cold spills it costs (MP=40: 4 waves,
  * 12 VGPRs spilled, 9 % faster than the unconstrained 3 waves) */
-#define CSS_MDS_WAVES(MP) ((MP) <= 24 ? 5 : (MP) <= 40 ? 4 : (MP) <= 64 ? 2 : 1)
+#define CSS_MDS_WAVES(MP) ((MP) <= 24 ? 5 : (MP) <= 40 ? 4 : (MP) <= 64 ? 2 : (MP) <= 96 ? 3 : 2)
 
 namespace {
 
@@ -285,15 +285,35 @@ __global__ void __launch_bounds__(256) k_css_pack(const gd_chrom_dev *ch, const 
 }
 
 /* ------------------------------------------------------------------------ */
-/* per-window classical MDS + CSS                                              */
+/* per-window classical MDS + CSS.  Matrix row i lives in the VGPRs of G lanes  */
+/* (t = G*i + h holds columns [h*CP, (h+1)*CP), CP = MP/G): G = 1 up to 64      */
+/* individuals, G = 2 above (half the registers per lane, 3x the occupancy).    */
+/* Row-level values (row sums, x_i, p_i, v_i, w_i, y_i) are replicated in the G */
+/* lanes of a row and counted once ("lead" lane) in block reductions.           */
 /* ------------------------------------------------------------------------ */
-template <int MP>
-__global__ void __launch_bounds__(64 * ((MP + 63) / 64), CSS_MDS_WAVES(MP))
+template <int MP, int G>
+struct CssShape {
+  static constexpr int CP = MP / G;
+  static constexpr int NT = 64 * ((MP * G + 63) / 64);
+  static constexpr int NW = NT / 64;
+};
+
+/* sum over the G lanes of a row (adjacent lanes) */
+template <int G>
+__device__ __forceinline__ double pair_sum(double x) {
+  if constexpr (G == 1)
+    return x;
+  else
+    return x + dpp64<0xB1, 0xF>(x, 0.0); /* quad_perm [1,0,3,2]: the partner lane */
+}
+
+template <int MP, int G>
+__global__ void __launch_bounds__((CssShape<MP, G>::NT), CSS_MDS_WAVES(MP))
     k_css_mds(const gd_chrom_dev *ch, int nchrom, const gd_css_planes *pl, const uint32_t *planes,
               const int32_t *lo_a_, const int32_t *hi_a_, const int32_t *lo_b_, const double *avals,
               const double *bvals, int64_t wtotal, int want_x, int force_literal, double *scores, double *pvals,
               double *xbuf, uint8_t *status, unsigned *flags) {
-  constexpr int NW = (MP + 63) / 64;
+  constexpr int CP = CssShape<MP, G>::CP, NT = CssShape<MP, G>::NT, NW = CssShape<MP, G>::NW;
   __shared__ double s_row[MP + 2];
   __shared__ double s_v[MP], s_w[MP];
   __shared__ __attribute__((aligned(16))) double s_d[MP + 4];
@@ -309,9 +329,12 @@ __global__ void __launch_bounds__(64 * ((MP + 63) / 64), CSS_MDS_WAVES(MP))
   __shared__ double s_lam[2];
   __shared__ double s_red[2 * NW];
 
-  const int i = threadIdx.x;
+  const int tid = threadIdx.x;
+  const int i = tid / G, h = tid % G; /* row, column part */
+  const int c0 = h * CP;              /* first column held by this lane */
+  const bool lead = h == 0;
   const int ii = i < MP ? i : MP - 1; /* clamped LDS index for lanes past MP */
-  if (i < MP) s_tr[i] = i;
+  if (tid < MP) s_tr[tid] = tid;
 
   /* one workgroup per window (no persistent loop: hoisting per-lane invariants out of
    * a window loop costs ~100 VGPRs and halves the occupancy) */
@@ -325,11 +348,11 @@ __global__ void __launch_bounds__(64 * ((MP + 63) / 64), CSS_MDS_WAVES(MP))
     const int npos = (ha - la) / a;
     if (npos <= 0) continue;
     if ((int64_t)lb + (int64_t)npos * b > d.blen) {
-      if (i == 0) atomicOr(flags, GD_FLAG_B_BOUNDS);
+      if (tid == 0) atomicOr(flags, GD_FLAG_B_BOUNDS);
       continue;
     }
     if (m > MP) {
-      if (i == 0) atomicOr(flags, GD_FLAG_BAD_SIZE);
+      if (tid == 0) atomicOr(flags, GD_FLAG_BAD_SIZE);
       continue;
     }
     const bool row = i < m;
@@ -341,7 +364,7 @@ __global__ void __launch_bounds__(64 * ((MP + 63) / 64), CSS_MDS_WAVES(MP))
     bool literal = force_literal || (la % a) != 0 || (lb % b) != 0;
     if (!literal) {
       int irr = 0;
-      for (int k = i; k * 64 < npos; k += 64 * NW) {
+      for (int k = tid; k * 64 < npos; k += NT) {
         const int nb = min(64, npos - 64 * k);
         const uint64_t tail = nb == 64 ? ~0ull : ((1ull << nb) - 1);
         const uint64_t xa = plane_bits64(pa + (int64_t)(2 * a) * P.wa, ra + 64 * k) & tail;
@@ -351,36 +374,37 @@ __global__ void __launch_bounds__(64 * ((MP + 63) / 64), CSS_MDS_WAVES(MP))
       literal = __syncthreads_or(irr);
     }
 
-    /* ---- compare_all: D[i][j] in registers, lane i = row i */
-    double A[MP];
+    /* ---- compare_all: D[i][c0 + jj] in registers */
+    double A[CP];
     {
-      int acc[MP];
+      int acc[CP];
 #pragma unroll
-      for (int j = 0; j < MP; ++j) acc[j] = 0;
+      for (int jj = 0; jj < CP; ++jj) acc[jj] = 0;
       if (!literal) {
         for (int k = 0; k * 64 < npos; ++k) {
           const int nb = min(64, npos - 64 * k);
           const uint64_t tail = nb == 64 ? ~0ull : ((1ull << nb) - 1);
           __syncthreads();
-          if (row) {
+          if (lead && row) {
             const uint32_t *base = i < a ? pa + (int64_t)(2 * i) * P.wa : pb + (int64_t)(2 * (i - a)) * P.wb;
             const int64_t nw = i < a ? P.wa : P.wb;
             const int64_t r = (i < a ? ra : rb) + 64 * k;
             s_mask[2 * i] = plane_bits64(base, r) & tail;
             s_mask[2 * i + 1] = plane_bits64(base + nw, r) & tail;
-          } else if (i < MP) {
+          } else if (lead && i < MP) {
             s_mask[2 * i] = 0;
             s_mask[2 * i + 1] = 0;
           }
           __syncthreads();
           const uint64_t Pi = s_mask[2 * ii], Ni = s_mask[2 * ii + 1];
 #pragma unroll
-          for (int j = 0; j < MP; ++j) {
+          for (int jj = 0; jj < CP; ++jj) {
+            const int j = c0 + jj;
             const uint64_t Pj = s_mask[2 * j], Nj = s_mask[2 * j + 1];
-            acc[j] += __popcll(Pi & Nj) + __popcll(Ni & Pj);
-            if ((j & 7) == 7) {
+            acc[jj] += __popcll(Pi & Nj) + __popcll(Ni & Pj);
+            if ((jj & 7) == 7) {
 #pragma unroll
-              for (int u = j - 7; u <= j; ++u) CSS_PIN(acc[u]);
+              for (int u = jj - 7; u <= jj; ++u) CSS_PIN(acc[u]);
             }
           }
         }
@@ -388,15 +412,17 @@ __global__ void __launch_bounds__(64 * ((MP + 63) / 64), CSS_MDS_WAVES(MP))
         const double *av = avals + d.a_off + la, *bv = bvals + d.b_off + lb;
         for (int k = 0; k < npos; ++k) {
           __syncthreads();
-          if (row) s_vals[i] = i < a ? av[(int64_t)k * a + i] : bv[(int64_t)k * b + (i - a)];
+          if (lead && row) s_vals[i] = i < a ? av[(int64_t)k * a + i] : bv[(int64_t)k * b + (i - a)];
           __syncthreads();
           const double vi = s_vals[ii];
-          int io = i, mo = m, ao = a;
+          int io = i, mo = m, ao = a, co = c0;
           CSS_OPAQUE_V(io);
+          CSS_OPAQUE_V(co);
           CSS_OPAQUE_S(mo);
           CSS_OPAQUE_S(ao);
 #pragma unroll
-          for (int j = 0; j < MP; ++j) {
+          for (int jj = 0; jj < CP; ++jj) {
+            const int j = co + jj;
             /* the diagonal never counts: (int)v * v >= 0 */
             if (j < mo) {
               const double vj = s_vals[j];
@@ -404,7 +430,7 @@ __global__ void __launch_bounds__(64 * ((MP + 63) / 64), CSS_MDS_WAVES(MP))
                * population and the A element across populations (css.c:281-326) */
               const bool cast_i = ((io < ao) == (j < ao)) ? (io > j) : (io < ao);
               const double prod = cast_i ? x86_int(vi) * vj : x86_int(vj) * vi;
-              acc[j] += prod == -9.0;
+              acc[jj] += prod == -9.0;
             }
           }
         }
@@ -412,7 +438,7 @@ __global__ void __launch_bounds__(64 * ((MP + 63) / 64), CSS_MDS_WAVES(MP))
       int mo = m;
       CSS_OPAQUE_S(mo);
 #pragma unroll
-      for (int j = 0; j < MP; ++j) A[j] = (row && j < mo) ? (double)acc[j] : 0.0;
+      for (int jj = 0; jj < CP; ++jj) A[jj] = (row && c0 + jj < mo) ? (double)acc[jj] : 0.0;
     }
 
     CSS_PROF(0);
@@ -423,12 +449,12 @@ __global__ void __launch_bounds__(64 * ((MP + 63) / 64), CSS_MDS_WAVES(MP))
       int mo = m;
       CSS_OPAQUE_S(mo);
 #pragma unroll
-      for (int j = 0; j < MP; ++j) {
-        if (row && j < mo) {
-          if (A[j] < 0.00001)
+      for (int jj = 0; jj < CP; ++jj) {
+        if (row && c0 + jj < mo) {
+          if (A[jj] < 0.00001)
             ++unval;
           else
-            sum += A[j];
+            sum += A[jj];
         }
       }
       double unv = (double)unval;
@@ -442,7 +468,7 @@ __global__ void __launch_bounds__(64 * ((MP + 63) / 64), CSS_MDS_WAVES(MP))
        * kept alive across the reduction); padding columns are re-zeroed below */
       CSS_OPAQUE_ROW(A);
 #pragma unroll
-      for (int j = 0; j < MP; ++j) A[j] = fma(avg, 1.0 - fmin(A[j], 1.0), A[j]);
+      for (int jj = 0; jj < CP; ++jj) A[jj] = fma(avg, 1.0 - fmin(A[jj], 1.0), A[jj]);
     }
 
     /* ---- B = -1/2 Z (D o D) Z, Z = I - 11^T/m, by double centering */
@@ -452,27 +478,28 @@ __global__ void __launch_bounds__(64 * ((MP + 63) / 64), CSS_MDS_WAVES(MP))
       int mo = m;
       CSS_OPAQUE_S(mo);
 #pragma unroll
-      for (int j = 0; j < MP; ++j) {
-        A[j] = (row && j < mo) ? A[j] * A[j] : 0.0;
-        rs += A[j];
+      for (int jj = 0; jj < CP; ++jj) {
+        A[jj] = (row && c0 + jj < mo) ? A[jj] * A[jj] : 0.0;
+        rs += A[jj];
       }
+      rs = pair_sum<G>(rs);
       const double ri = row ? rs / m : 0.0;
       __syncthreads();
-      if (i < MP) s_v[i] = ri;
-      const double g = block_sum<NW>(ri, s_red) / m;
+      if (lead && i < MP) s_v[i] = ri;
+      const double g = block_sum<NW>(lead ? ri : 0.0, s_red) / m;
       __syncthreads();
       CSS_OPAQUE_S(mo);
 #pragma unroll
-      for (int j = 0; j < MP; ++j) {
-        A[j] = (row && j < mo) ? -0.5 * ((A[j] - (ri + s_v[j])) + g) : 0.0;
-        if ((j & 7) == 7) {
+      for (int jj = 0; jj < CP; ++jj) {
+        A[jj] = (row && c0 + jj < mo) ? -0.5 * ((A[jj] - (ri + s_v[c0 + jj])) + g) : 0.0;
+        if ((jj & 7) == 7) {
 #pragma unroll
-          for (int u = j - 7; u <= j; ++u) CSS_PIN(A[u]);
+          for (int u = jj - 7; u <= jj; ++u) CSS_PIN(A[u]);
         }
       }
       double f2 = 0;
 #pragma unroll
-      for (int j = 0; j < MP; ++j) f2 = fma(A[j], A[j], f2);
+      for (int jj = 0; jj < CP; ++jj) f2 = fma(A[jj], A[jj], f2);
       /* eigenvalues within rounding of 0 count as 0 (oracle/css_oracle.c, cmds) */
       zero_tol = 64.0 * m * DBL_EPSILON * sqrt(block_sum<NW>(f2, s_red));
     }
@@ -480,50 +507,53 @@ __global__ void __launch_bounds__(64 * ((MP + 63) / 64), CSS_MDS_WAVES(MP))
     CSS_PROF(1);
     /* ---- Householder tridiagonalisation (LAPACK dsytd2, lower).  Column k of the
      * trailing matrix is read from row k (symmetry); after step k the dead column k
-     * of each row holds that row's element of the reflector v_k. */
+     * of each row holds that row's element of the reflector v_k.  Columns are
+     * handled in blocks of 8; a block dead in every column part (v, w and x are 0
+     * left of k) is skipped by a uniform branch. */
     for (int k = 0; k < m; ++k) {
       __syncthreads();
-      /* Columns are handled in blocks of 8; blocks entirely left of k are dead
-       * (their v and w entries are 0) and skipped by a uniform branch.  Lane k
-       * publishes x = row k right of the diagonal (zeros at j <= k) and d_k. */
+      /* row k's lanes publish x = row k right of the diagonal (zeros at j <= k) and d_k */
       if (i == k) {
 #pragma unroll
-        for (int jb = 0; jb < MP / 8; ++jb)
-          if (8 * jb + 7 >= k) {
+        for (int jb = 0; jb < CP / 8; ++jb)
+          if ((G - 1) * CP + 8 * jb + 7 >= k) {
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
-              const int j = 8 * jb + u;
-              s_row[j] = j > k ? A[j] : 0.0;
-              if (j == k) s_d[k] = A[j];
+              const int j = c0 + 8 * jb + u;
+              s_row[j] = j > k ? A[8 * jb + u] : 0.0;
+              if (j == k) s_d[k] = A[8 * jb + u];
             }
           }
       }
       __syncthreads();
       if (k >= m - 2) {
-        if (i == 0 && k == m - 2) s_e[k] = s_row[k + 1];
+        if (tid == 0 && k == m - 2) s_e[k] = s_row[k + 1];
         continue;
       }
       const double xi = (i > k + 1 && row) ? s_row[ii] : 0.0;
       const double alpha = s_row[k + 1];
       /* A x and A e_{k+1} need only x, so they overlap the norm reduction */
+      const int lk1 = k + 1 - c0; /* column k+1 in this lane's part, if there */
       double p0 = 0, p1 = 0, ak1 = 0;
 #pragma unroll
-      for (int jb = 0; jb < MP / 8; ++jb) {
-        if (8 * jb + 7 > k) {
+      for (int jb = 0; jb < CP / 8; ++jb) {
+        if ((G - 1) * CP + 8 * jb + 7 > k) {
 #pragma unroll
           for (int u = 0; u < 8; u += 2) {
-            p0 = fma(A[8 * jb + u], s_row[8 * jb + u], p0);
-            p1 = fma(A[8 * jb + u + 1], s_row[8 * jb + u + 1], p1);
+            p0 = fma(A[8 * jb + u], s_row[c0 + 8 * jb + u], p0);
+            p1 = fma(A[8 * jb + u + 1], s_row[c0 + 8 * jb + u + 1], p1);
           }
           CSS_PIN(p0);
           CSS_PIN(p1);
         }
-        if (((k + 1) >> 3) == jb) {
+        if ((lk1 >> 3) == jb) {
 #pragma unroll
-          for (int u = 0; u < 8; ++u) ak1 = (8 * jb + u == k + 1) ? A[8 * jb + u] : ak1;
+          for (int u = 0; u < 8; ++u) ak1 = (8 * jb + u == lk1) ? A[8 * jb + u] : ak1;
         }
       }
-      const double sigma = block_sum<NW>(xi * xi, s_red);
+      const double sigma = block_sum<NW>(lead ? xi * xi : 0.0, s_red);
+      const double praw = pair_sum<G>(p0 + p1);
+      ak1 = pair_sum<G>(ak1);
       double tau = 0.0, beta = alpha, scale = 0.0;
       if (sigma != 0.0) {
         beta = -copysign(sqrt(alpha * alpha + sigma), alpha);
@@ -532,33 +562,34 @@ __global__ void __launch_bounds__(64 * ((MP + 63) / 64), CSS_MDS_WAVES(MP))
       }
       /* v = scale (x - beta e_{k+1}), v_{k+1} = 1;  p = tau A v */
       const double vi = (i == k + 1) ? 1.0 : xi * scale;
-      const double pi = (i > k && row) ? (tau * scale) * fma(-beta, ak1, p0 + p1) : 0.0;
-      const double K = -0.5 * tau * block_sum<NW>(pi * vi, s_red);
+      const double pi = (i > k && row) ? (tau * scale) * fma(-beta, ak1, praw) : 0.0;
+      const double K = -0.5 * tau * block_sum<NW>(lead ? pi * vi : 0.0, s_red);
       const double wi = fma(K, vi, pi);
-      if (i == 0) {
+      if (tid == 0) {
         s_e[k] = beta;
         s_tau[k] = tau;
       }
-      if (i < MP) {
+      if (lead && i < MP) {
         s_v[i] = vi;
         s_w[i] = wi;
       }
       __syncthreads();
+      const int lk = k - c0; /* the dead column k in this lane's part, if there */
 #pragma unroll
-      for (int jb = 0; jb < MP / 8; ++jb) {
-        if (8 * jb + 7 > k) {
+      for (int jb = 0; jb < CP / 8; ++jb) {
+        if ((G - 1) * CP + 8 * jb + 7 > k) {
 #pragma unroll
           for (int u = 0; u < 8; ++u) {
-            const int j = 8 * jb + u;
-            A[j] = fma(-vi, s_w[j], fma(-wi, s_v[j], A[j]));
+            const int j = c0 + 8 * jb + u;
+            A[8 * jb + u] = fma(-vi, s_w[j], fma(-wi, s_v[j], A[8 * jb + u]));
           }
 #pragma unroll
           for (int u = 0; u < 8; ++u) CSS_PIN(A[8 * jb + u]);
         }
         /* stash v_k in the dead column k */
-        if ((k >> 3) == jb) {
+        if ((lk >> 3) == jb) {
 #pragma unroll
-          for (int u = 0; u < 8; ++u) A[8 * jb + u] = (8 * jb + u == k) ? vi : A[8 * jb + u];
+          for (int u = 0; u < 8; ++u) A[8 * jb + u] = (8 * jb + u == lk) ? vi : A[8 * jb + u];
         }
       }
     }
@@ -572,28 +603,28 @@ __global__ void __launch_bounds__(64 * ((MP + 63) / 64), CSS_MDS_WAVES(MP))
     double glo, ghi;
     {
       double lo = DBL_MAX, hi = -DBL_MAX;
-      if (row) {
+      if (lead && row) {
         const double r = (i > 0 ? fabs(s_e[i - 1]) : 0.0) + (i < m - 1 ? fabs(s_e[i]) : 0.0);
         lo = s_d[i] - r;
         hi = s_d[i] + r;
       }
-      if (i < MP + 4) {
+      if (tid < MP + 4) {
         /* Sturm arrays: s_e2[k] = e_{k-1}^2 (s_e2[0] = 0); entries m..m4 are a
          * decoupled tail far above the spectrum (no sign changes) */
-        s_e2[i] = (i >= 1 && i < m) ? s_e[i - 1] * s_e[i - 1] : 0.0;
+        s_e2[tid] = (tid >= 1 && tid < m) ? s_e[tid - 1] * s_e[tid - 1] : 0.0;
       }
       glo = block_reduce<NW, OpMin>(lo, s_red);
       ghi = block_reduce<NW, OpMax>(hi, s_red);
       const double pad = 2.0 * DBL_EPSILON * fmax(fabs(glo), fabs(ghi)) * m + DBL_MIN;
       glo -= pad;
       ghi += pad;
-      if (i >= m && i < MP + 4) s_d[i] = 2.0 * fabs(ghi) + 2.0 * fabs(glo) + 1.0;
+      if (tid >= m && tid < MP + 4) s_d[tid] = 2.0 * fabs(ghi) + 2.0 * fabs(glo) + 1.0;
     }
     const int m4 = (m + 3) & ~3;
     __syncthreads();
-    if (i < 64) {
-      const int h = i >> 5, j = i & 31;
-      const int target = m - 1 - h; /* ascending index of the eigenvalue */
+    if (tid < 64) {
+      const int hh = tid >> 5, j = tid & 31;
+      const int target = m - 1 - hh; /* ascending index of the eigenvalue */
       double l = glo, u = ghi;
       for (int it = 0; it < 80; ++it) {
         const double x = l + (u - l) * ((double)(j + 1) * (1.0 / 33.0));
@@ -609,8 +640,8 @@ __global__ void __launch_bounds__(64 * ((MP + 63) / 64), CSS_MDS_WAVES(MP))
           const double dk[4] = {d01.x, d01.y, d23.x, d23.y};
           const double ek[4] = {e01.x, e01.y, e23.x, e23.y}; /* e_{k-1}^2, s_e2[0] = 0 */
 #pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            double pn = fma(dk[u] - x, pc, -(ek[u] * pm));
+          for (int uu = 0; uu < 4; ++uu) {
+            double pn = fma(dk[uu] - x, pc, -(ek[uu] * pm));
             /* an exactly zero minor takes the sign opposite to its predecessor */
             pn = (pn == 0.0) ? -pc * DBL_MIN : pn;
             cnt += (int)((__double2hiint(pn) ^ __double2hiint(pc)) < 0);
@@ -637,60 +668,59 @@ __global__ void __launch_bounds__(64 * ((MP + 63) / 64), CSS_MDS_WAVES(MP))
       }
       if (j == 0) {
         const double lam = 0.5 * (l + u);
-        s_lam[h] = fabs(lam) <= zero_tol ? 0.0 : lam;
+        s_lam[hh] = fabs(lam) <= zero_tol ? 0.0 : lam;
       }
     }
     __syncthreads();
 
     CSS_PROF(3);
     /* ---- eigenvectors of T: two steps of inverse iteration with a partial-pivot
-     * LU of T - lam I (lane 0: largest, lane 1: second).  The serial chains carry
+     * LU of T - lam I (thread 0: largest, thread 1: second).  The serial chains carry
      * their running values in registers; LDS holds only read-once factors. */
-    if (i < 2) {
-      const double sig = s_lam[i];
-      const double tiny = DBL_EPSILON * fmax(fmax(fabs(glo), fabs(ghi)), DBL_MIN);
-      double *U0 = s_lu[i][0], *U1 = s_lu[i][1], *U2 = s_lu[i][2];
-      double *ml = s_x + i * MP; /* elimination multipliers; s_x is free until X is formed */
-      uint8_t *pv = s_piv[i];
-      double c0 = s_d[0] - sig, c1 = m > 1 ? s_e[0] : 0.0;
+    if (tid < 2) {
+      const double sig = s_lam[tid];
+      double *U0 = s_lu[tid][0], *U1 = s_lu[tid][1], *U2 = s_lu[tid][2];
+      double *ml = s_x + tid * MP; /* elimination multipliers; s_x is free until X is formed */
+      uint8_t *pv = s_piv[tid];
+      double cc0 = s_d[0] - sig, cc1 = m > 1 ? s_e[0] : 0.0;
       for (int k = 0; k < m - 1; ++k) {
         const double n0 = s_e[k], n1 = s_d[k + 1] - sig, n2 = (k + 2 < m) ? s_e[k + 1] : 0.0;
-        const bool sw = fabs(c0) < fabs(n0);
-        const double pvt = sw ? n0 : c0, oth = sw ? c0 : n0;
+        const bool sw = fabs(cc0) < fabs(n0);
+        const double pvt = sw ? n0 : cc0, oth = sw ? cc0 : n0;
         const double t = (pvt != 0.0) ? oth * fast_rcp(pvt) : 0.0;
         U0[k] = pvt;
-        U1[k] = sw ? n1 : c1;
+        U1[k] = sw ? n1 : cc1;
         U2[k] = sw ? n2 : 0.0;
         ml[k] = t;
         pv[k] = sw;
-        const double nc0 = sw ? fma(-t, n1, c1) : fma(-t, c1, n1);
-        c1 = sw ? -t * n2 : n2;
-        c0 = nc0;
+        const double nc0 = sw ? fma(-t, n1, cc1) : fma(-t, cc1, n1);
+        cc1 = sw ? -t * n2 : n2;
+        cc0 = nc0;
       }
-      U0[m - 1] = c0;
+      U0[m - 1] = cc0;
       /* start vector: deterministic, not orthogonal to anything in practice */
       for (int k = 0; k < m; ++k) {
-        const double f = (double)((k * 40503u + 977u * (unsigned)(i + 1)) & 1023u) / 1024.0;
-        s_y[i][k] = (i == 0 ? 1.0 : ((k & 1) ? -1.0 : 1.0)) * (0.5 + f);
+        const double f = (double)((k * 40503u + 977u * (unsigned)(tid + 1)) & 1023u) / 1024.0;
+        s_y[tid][k] = (tid == 0 ? 1.0 : ((k & 1) ? -1.0 : 1.0)) * (0.5 + f);
       }
     }
     __syncthreads();
-    if (row) {
+    if (tid < m) {
       /* reciprocal pivots, in parallel (zero pivots -> tiny) */
       const double tiny = DBL_EPSILON * fmax(fmax(fabs(glo), fabs(ghi)), DBL_MIN);
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const double u0 = s_lu[h][0][i];
-        s_lu[h][0][i] = fast_rcp(u0 == 0.0 ? tiny : u0);
+      for (int e = 0; e < 2; ++e) {
+        const double u0 = s_lu[e][0][tid];
+        s_lu[e][0][tid] = fast_rcp(u0 == 0.0 ? tiny : u0);
       }
     }
     double y1 = 0.0, y2 = 0.0;
     for (int itn = 0; itn < 2; ++itn) {
       __syncthreads();
-      if (i < 2) {
-        double *y = s_y[i];
-        const double *R0 = s_lu[i][0], *U1 = s_lu[i][1], *U2 = s_lu[i][2], *ml = s_x + i * MP;
-        const uint8_t *pv = s_piv[i];
+      if (tid < 2) {
+        double *y = s_y[tid];
+        const double *R0 = s_lu[tid][0], *U1 = s_lu[tid][1], *U2 = s_lu[tid][2], *ml = s_x + tid * MP;
+        const uint8_t *pv = s_piv[tid];
         double yk = y[0];
         for (int k = 0; k < m - 1; ++k) {
           double yn = y[k + 1];
@@ -714,34 +744,39 @@ __global__ void __launch_bounds__(64 * ((MP + 63) / 64), CSS_MDS_WAVES(MP))
       __syncthreads();
       y1 = row ? s_y[0][ii] : 0.0;
       y2 = row ? s_y[1][ii] : 0.0;
-      double n1 = y1 * y1, n2 = y2 * y2;
+      double n1 = lead ? y1 * y1 : 0.0, n2 = lead ? y2 * y2 : 0.0;
       block_sum2<NW>(n1, n2, s_red);
       y1 *= 1.0 / sqrt(n1);
       y2 *= 1.0 / sqrt(n2);
-      if (itn == 0 && row) {
+      __syncthreads();
+      if (itn == 0 && lead && row) {
         s_y[0][i] = y1;
         s_y[1][i] = y2;
       }
     }
     /* orthogonalise the second vector against the first (close eigenvalues) */
     {
-      double dt = y1 * y2, zero = 0.0;
+      double dt = lead ? y1 * y2 : 0.0, zero = 0.0;
       block_sum2<NW>(dt, zero, s_red);
       y2 = fma(-dt, y1, y2);
-      double n2 = y2 * y2;
+      double n2 = lead ? y2 * y2 : 0.0;
       zero = 0.0;
       block_sum2<NW>(n2, zero, s_red);
       y2 *= 1.0 / sqrt(n2);
     }
 
     CSS_PROF(4);
-    /* ---- back-transformation y <- H_0 H_1 ... H_{m-3} y */
+    /* ---- back-transformation y <- H_0 H_1 ... H_{m-3} y; v_k sits in column k,
+     * i.e. in part k / CP of the row */
 #pragma unroll
     for (int k = MP - 3; k >= 0; --k) {
       if (k <= m - 3) {
-        const double vk = row ? A[k] : 0.0;
+        constexpr int dummy = 0;
+        (void)dummy;
+        const int hk = k / CP, lk = k - hk * CP;
+        const double vk = pair_sum<G>((row && h == hk) ? A[lk] : 0.0);
         const double t = s_tau[k];
-        double d1 = vk * y1, d2 = vk * y2;
+        double d1 = lead ? vk * y1 : 0.0, d2 = lead ? vk * y2 : 0.0;
         block_sum2<NW>(d1, d2, s_red);
         y1 = fma(-(t * d1), vk, y1);
         y2 = fma(-(t * d2), vk, y2);
@@ -754,7 +789,7 @@ __global__ void __launch_bounds__(64 * ((MP + 63) / 64), CSS_MDS_WAVES(MP))
     {
       const double L1 = sqrt(s_lam[0]), L2 = sqrt(s_lam[1]);
       __syncthreads();
-      if (row) {
+      if (lead && row) {
         s_x[2 * i] = y1 * L1 + y2 * 0.0;
         s_x[2 * i + 1] = y1 * 0.0 + y2 * L2;
       }
@@ -763,14 +798,13 @@ __global__ void __launch_bounds__(64 * ((MP + 63) / 64), CSS_MDS_WAVES(MP))
     const double score = css_score<NW>(s_tr, a, b, [&](int p, int q) { return xdist(s_x, p, q); }, s_red);
     CSS_PROF(6);
     if (score == -1.0) continue; /* the reference's "discarded" marker (css.c:127) */
-    if (i == 0) {
+    if (tid == 0) {
       scores[d.w_out + wl] = score;
       if (!want_x) pvals[d.w_out + wl] = 1.0; /* runs == 0: p = (0 + 1) / (0 + 1) */
     }
     if (want_x) {
-      if (i < 2 * MP) xbuf[w * 2 * MP + i] = (i < 2 * m) ? s_x[i] : 0.0;
-      if (i + 64 * NW < 2 * MP) xbuf[w * 2 * MP + i + 64 * NW] = (i + 64 * NW < 2 * m) ? s_x[i + 64 * NW] : 0.0;
-      if (i == 0) status[w] = 1;
+      for (int e = tid; e < 2 * MP; e += NT) xbuf[w * 2 * MP + e] = (e < 2 * m) ? s_x[e] : 0.0;
+      if (tid == 0) status[w] = 1;
     }
   }
 }
@@ -931,27 +965,28 @@ __global__ void __launch_bounds__(64 * ((MP + 63) / 64))
 
 /* ------------------------------------------------------------------------ */
 int gd_css_tier(int m) {
-  static const int tiers[] = {24, 40, 64, 80, 96};
+  static const int tiers[] = {24, 40, 64, 80, 96, 128};
   for (int t : tiers)
     if (m <= t) return t;
   return 0;
 }
 
-template <int MP>
+template <int MP, int G>
 static int launch_tier(const gd_chrom_dev *d_ch, int nchrom, const gd_css_planes *d_pl, const uint32_t *planes,
                        const int32_t *lo_a, const int32_t *hi_a, const int32_t *lo_b, const double *avals,
                        const double *bvals, int64_t wtotal, int treshold, int runs, double *scores, double *p,
                        double *xbuf, uint8_t *status, unsigned *flags, hipStream_t s) {
-  constexpr int NT = 64 * ((MP + 63) / 64);
+  constexpr int NT = CssShape<MP, G>::NT;
   const int want_x = (runs > 0 && treshold > 0) ? 1 : 0;
   const unsigned gx = (unsigned)wtotal;
   const char *fl = getenv("GD_CSS_FORCE_LITERAL"); /* diagnostics: per-SNP predicate for every window */
   const int force_literal = (fl && fl[0] == '1') ? 1 : 0;
-  hipLaunchKernelGGL(k_css_mds<MP>, dim3(gx), dim3(NT), 0, s, d_ch, nchrom, d_pl, planes, lo_a, hi_a, lo_b, avals,
+  hipLaunchKernelGGL((k_css_mds<MP, G>), dim3(gx), dim3(NT), 0, s, d_ch, nchrom, d_pl, planes, lo_a, hi_a, lo_b, avals,
                      bvals, wtotal, want_x, force_literal, scores, p, xbuf, status, flags);
   if (hipGetLastError() != hipSuccess) return GD_ERR_HIP;
   if (want_x) {
-    hipLaunchKernelGGL(k_css_perm<MP>, dim3((unsigned)std::min<int64_t>(wtotal, 256 * 32)), dim3(NT), 0, s, d_ch, nchrom, xbuf, status, wtotal,
+    hipLaunchKernelGGL(k_css_perm<MP>, dim3((unsigned)std::min<int64_t>(wtotal, 256 * 32)),
+                       dim3(64 * ((MP + 63) / 64)), 0, s, d_ch, nchrom, xbuf, status, wtotal,
                        treshold, runs, p);
     if (hipGetLastError() != hipSuccess) return GD_ERR_HIP;
   }
@@ -987,20 +1022,23 @@ int gd_css_launch(int mp, const gd_chrom_dev *d_ch, int nchrom, const gd_css_pla
 #endif
   switch (mp) {
     case 24:
-      return launch_tier<24>(d_ch, nchrom, d_pl, planes, lo_a, hi_a, lo_b, avals, bvals, wtotal, treshold, runs,
+      return launch_tier<24, 1>(d_ch, nchrom, d_pl, planes, lo_a, hi_a, lo_b, avals, bvals, wtotal, treshold, runs,
                              scores, p, xbuf, status, flags, s);
     case 40:
-      return launch_tier<40>(d_ch, nchrom, d_pl, planes, lo_a, hi_a, lo_b, avals, bvals, wtotal, treshold, runs,
+      return launch_tier<40, 1>(d_ch, nchrom, d_pl, planes, lo_a, hi_a, lo_b, avals, bvals, wtotal, treshold, runs,
                              scores, p, xbuf, status, flags, s);
     case 64:
-      return launch_tier<64>(d_ch, nchrom, d_pl, planes, lo_a, hi_a, lo_b, avals, bvals, wtotal, treshold, runs,
+      return launch_tier<64, 1>(d_ch, nchrom, d_pl, planes, lo_a, hi_a, lo_b, avals, bvals, wtotal, treshold, runs,
                              scores, p, xbuf, status, flags, s);
     case 80:
-      return launch_tier<80>(d_ch, nchrom, d_pl, planes, lo_a, hi_a, lo_b, avals, bvals, wtotal, treshold, runs,
+      return launch_tier<80, 2>(d_ch, nchrom, d_pl, planes, lo_a, hi_a, lo_b, avals, bvals, wtotal, treshold, runs,
                              scores, p, xbuf, status, flags, s);
     case 96:
-      return launch_tier<96>(d_ch, nchrom, d_pl, planes, lo_a, hi_a, lo_b, avals, bvals, wtotal, treshold, runs,
+      return launch_tier<96, 2>(d_ch, nchrom, d_pl, planes, lo_a, hi_a, lo_b, avals, bvals, wtotal, treshold, runs,
                              scores, p, xbuf, status, flags, s);
+    case 128:
+      return launch_tier<128, 2>(d_ch, nchrom, d_pl, planes, lo_a, hi_a, lo_b, avals, bvals, wtotal, treshold,
+                                 runs, scores, p, xbuf, status, flags, s);
   }
   return GD_ERR_SIZE;
 }

@@ -112,7 +112,7 @@ def test_unsupported_options_raise():
 
 def test_cohort_above_largest_tier_raises():
     from gdscan import GdError, css
-    av, bv, ap, bp, regend = _synth(10, 3_000, 60, 40)
+    av, bv, ap, bp, regend = _synth(10, 2_000, 70, 70)
     with pytest.raises(GdError):
         css.scan(av, bv, ap, bp, regend)
 
