@@ -90,6 +90,54 @@ def css_cpu_baseline(args):
                       f"absent here)"}
 
 
+def css_shape_run(args, lib, _lib, synth, Chrom, check, dev, stream, ctx, rank, nchrom, pop, treshold, runs):
+    """One timed CSS scan of `nchrom` synthetic chromosomes with pop+pop individuals."""
+    import torch
+    nsnp = args.nsnp
+    alen = nsnp * pop
+    av = torch.empty(nchrom * alen, dtype=torch.float64, device=dev)
+    bv = torch.empty(nchrom * alen, dtype=torch.float64, device=dev)
+    ap = torch.empty(nchrom * alen, dtype=torch.int32, device=dev)
+    bp = torch.empty(nchrom * alen, dtype=torch.int32, device=dev)
+    qtab = torch.from_numpy(synth.freq_table()).to(dev)
+    for c in range(nchrom):
+        check(lib.gd_synth_device(1000 + rank * nchrom + c, nsnp, pop, pop, synth.MASTER_SEED, qtab.data_ptr(),
+                                  av.data_ptr() + c * alen * 8, bv.data_ptr() + c * alen * 8,
+                                  ap.data_ptr() + c * alen * 4, bp.data_ptr() + c * alen * 4, stream))
+    torch.cuda.synchronize()
+    last = ap.view(nchrom, alen)[:, -1].cpu().numpy().astype(np.int64)
+    chroms = (Chrom * nchrom)()
+    w_out = windows = 0
+    for c in range(nchrom):
+        regend = int(last[c]) + 1
+        chroms[c].a_off = chroms[c].b_off = c * alen
+        chroms[c].alen = chroms[c].blen = alen
+        chroms[c].regend = regend
+        chroms[c].w_out = w_out
+        chroms[c].seed = synth.MASTER_SEED + 1000 + c
+        w_out += regend // args.wstep
+        windows += lib.gd_window_count(regend, args.wsize, args.wstep, _lib.GD_WINDOWS_THREADED)
+    sc = torch.zeros(w_out, dtype=torch.float64, device=dev)
+    pv = torch.zeros_like(sc)
+
+    def step():
+        check(lib.gd_css_scan_device(ctx, chroms, nchrom, av.data_ptr(), bv.data_ptr(), ap.data_ptr(), bp.data_ptr(),
+                                     args.wsize, args.wstep, treshold, runs, _lib.GD_WINDOWS_THREADED,
+                                     sc.data_ptr(), pv.data_ptr(), stream))
+
+    step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    step()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    pm = pv.cpu().numpy()
+    computed = sc.cpu().numpy() != 0
+    return {"value": windows / dt, "unit": "windows/s (one GPU)", "ms": dt * 1e3, "windows": windows,
+            "config": f"{nchrom} chromosomes x {nsnp} SNPs, {pop}+{pop}, mcT={treshold}, mcR={runs}",
+            "mean_p": float(pm[computed].mean()) if computed.any() else None}
+
+
 def cpu_baseline(args):
     """Reference threadcompute() (64 pthreads) on a sample of the same workload."""
     from gdscan import synth
@@ -332,6 +380,13 @@ def main():
         }
         if rank == 0 and world == 1 and not args.no_cpu:
             out["css"]["cpu_baseline"] = css_cpu_baseline(args)
+        # the per-GPU shapes of configs[3] (40+40, runs=0) and configs[4] (40+40, mcT=10,
+        # mcR=1000) on a few chromosomes of their own: windows/s per GPU
+        del avals, bvals, apos, bpos
+        out["css"]["c4_shape"] = css_shape_run(args, lib, _lib, synth, Chrom, check, dev, stream, ctx, rank,
+                                               nchrom=4, pop=40, treshold=10, runs=0)
+        out["css"]["c5_shape"] = css_shape_run(args, lib, _lib, synth, Chrom, check, dev, stream, ctx, rank,
+                                               nchrom=1, pop=40, treshold=10, runs=1000)
     lib.gd_ctx_destroy(ctx)
     if rank == 0:
         print(json.dumps(out), flush=True)
