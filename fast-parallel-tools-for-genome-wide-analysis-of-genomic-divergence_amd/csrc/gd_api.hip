@@ -65,6 +65,7 @@ static int fail(int code, const std::string &msg) {
   g_err = msg;
   return code;
 }
+void gd_set_error(const char *msg) { g_err = msg ? msg : ""; } /* for gd_gtrack.cpp */
 
 #define HIP_TRY(expr)                                                                     \
   do {                                                                                    \
@@ -459,6 +460,89 @@ static int host_scan(const double *avals, const double *bvals, const int *apos, 
   }
   HIP_TRY(hipStreamSynchronize(s));
   return GD_OK;
+}
+
+static int css_scan_locked(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, const double *avals,
+                           const double *bvals, const int32_t *apos, const int32_t *bpos, int wsize, int wstep,
+                           int treshold, int runs, int window_set, double *scores, double *p, hipStream_t s);
+
+/* several chromosomes from host memory in one device scan: H2D of the inputs and of
+ * the caller's outputs (kept at uncomputed windows), the batched scan, D2H */
+template <class Run>
+static int host_batch(const gd_chrom *chroms, int nchrom, const double *avals, const double *bvals, const int *apos,
+                      const int *bpos, int wstep, double *out0, double *out1, Run run) {
+  if (nchrom < 0 || (nchrom > 0 && !chroms)) return fail(GD_ERR_ARG, "bad chromosome list");
+  if (wstep <= 0) return fail(GD_ERR_ARG, "wsize and wstep must be positive");
+  int64_t na = 0, nb = 0, nw = 0;
+  for (int c = 0; c < nchrom; ++c) {
+    const gd_chrom &h = chroms[c];
+    if (h.alen < 0 || h.blen < 0 || h.a_off < 0 || h.b_off < 0 || h.w_out < 0)
+      return fail(GD_ERR_ARG, "negative extent");
+    na = std::max<int64_t>(na, h.a_off + h.alen);
+    nb = std::max<int64_t>(nb, h.b_off + h.blen);
+    nw = std::max<int64_t>(nw, h.w_out + std::max(h.regend, 0) / wstep);
+  }
+  if (nchrom == 0 || nw == 0) return GD_OK;
+  if (!avals || !bvals || !apos || !bpos || !out0 || !out1) return fail(GD_ERR_ARG, "null buffer");
+  int st;
+  gd_ctx *ctx = default_ctx(&st);
+  if (!ctx) return fail(GD_ERR_HIP, "no HIP device available");
+  std::lock_guard<std::mutex> g(ctx->mu);
+  HIP_TRY(hipSetDevice(ctx->device));
+  Carve cv{nullptr};
+  auto lay = [&](Carve &k, double **av, double **bv, int32_t **ap, int32_t **bp, double **o0, double **o1) {
+    *av = k.take<double>(std::max<int64_t>(na, 1));
+    *bv = k.take<double>(std::max<int64_t>(nb, 1));
+    *ap = k.take<int32_t>(std::max<int64_t>(na, 1));
+    *bp = k.take<int32_t>(std::max<int64_t>(nb, 1));
+    *o0 = k.take<double>(nw);
+    *o1 = k.take<double>(nw);
+  };
+  double *av, *bv, *o0, *o1;
+  int32_t *ap, *bp;
+  lay(cv, &av, &bv, &ap, &bp, &o0, &o1);
+  if ((st = grow(&ctx->io, &ctx->io_cap, cv.off))) return st;
+  Carve real{ctx->io};
+  lay(real, &av, &bv, &ap, &bp, &o0, &o1);
+  hipStream_t s = ctx->stream;
+  if (na) {
+    HIP_TRY(hipMemcpyAsync(av, avals, sizeof(double) * na, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(ap, apos, sizeof(int32_t) * na, hipMemcpyHostToDevice, s));
+  }
+  if (nb) {
+    HIP_TRY(hipMemcpyAsync(bv, bvals, sizeof(double) * nb, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(bp, bpos, sizeof(int32_t) * nb, hipMemcpyHostToDevice, s));
+  }
+  HIP_TRY(hipMemcpyAsync(o0, out0, sizeof(double) * nw, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(o1, out1, sizeof(double) * nw, hipMemcpyHostToDevice, s));
+  st = run(ctx, av, bv, ap, bp, o0, o1, s);
+  if (st) return st;
+  HIP_TRY(hipMemcpyAsync(out0, o0, sizeof(double) * nw, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(out1, o1, sizeof(double) * nw, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  return GD_OK;
+}
+
+extern "C" int gd_fet_scan_host_batch(const gd_chrom *chroms, int nchrom, const double *avals, const double *bvals,
+                                      const int *apos, const int *bpos, int wsize, int wstep, double perc,
+                                      int window_set, double *scores, double *stddev) {
+  return host_batch(chroms, nchrom, avals, bvals, apos, bpos, wstep, scores, stddev,
+                    [&](gd_ctx *ctx, double *av, double *bv, int32_t *ap, int32_t *bp, double *o0, double *o1,
+                        hipStream_t s) {
+                      return fet_scan_locked(ctx, chroms, nchrom, av, bv, ap, bp, wsize, wstep, perc, window_set,
+                                             o0, o1, s);
+                    });
+}
+
+extern "C" int gd_css_scan_host_batch(const gd_chrom *chroms, int nchrom, const double *avals, const double *bvals,
+                                      const int *apos, const int *bpos, int wsize, int wstep, int treshold,
+                                      int runs, int window_set, double *scores, double *p) {
+  return host_batch(chroms, nchrom, avals, bvals, apos, bpos, wstep, scores, p,
+                    [&](gd_ctx *ctx, double *av, double *bv, int32_t *ap, int32_t *bp, double *o0, double *o1,
+                        hipStream_t s) {
+                      return css_scan_locked(ctx, chroms, nchrom, av, bv, ap, bp, wsize, wstep, treshold, runs,
+                                             window_set, o0, o1, s);
+                    });
 }
 
 extern "C" int gd_fet_scan_host(const double *avals, const double *bvals, const int *apos, const int *bpos,

@@ -1,0 +1,323 @@
+/*
+ * gd_gtrack.cpp -- HyperBrowser track I/O around the scan.
+ *
+ * Reader: GTrack "valued points" files as written by the reference's converter
+ * (tools/VCFConvert.py:44-86: header lines starting with '#', a "###" line naming the
+ * columns -- seqid, start, value, genomeid -- then one line per (SNP, individual) in
+ * population-list order).  Per seqid, in file order, it yields exactly the arrays
+ * HyperBrowser hands the statistics (startsAsNumpyArray -> int32, valsAsNumpyArray ->
+ * float64; FisherExactScoreStat.py:36-40).  The file is memory-mapped and parsed in one
+ * pass per chunk, chunks split at line boundaries and parsed on up to 16 threads;
+ * integer-valued tokens (all genotype codes) take a fast path, anything else goes
+ * through strtod.
+ *
+ * Writer: the tools' tabular result lines (FisherExactTestSNPTool.py:162-189,
+ * ClusterSeparationScore.py:180-205): "seqid\tstart\tscore\tstddev|p" for every window
+ * with score != 0, start = i * wStep, floats printed like Python 2's str(float)
+ * ('%.12g', plus ".0" when the text would read as an integer; quirk Q11).
+ */
+#include <cerrno>
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <algorithm>
+#include <string>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include "../../include/gdscan.h"
+
+void gd_set_error(const char *msg); /* gd_api.hip */
+
+struct gd_gtrack {
+  std::vector<std::string> seqid;
+  std::vector<std::vector<int32_t>> starts;
+  std::vector<std::vector<double>> vals;
+};
+
+namespace {
+
+struct Columns {
+  int seqid = 0, start = 1, value = 2, ncol = 4;
+};
+
+/* split [p, e) on tabs into at most `max` fields */
+int split_tabs(const char *p, const char *e, const char **fb, const char **fe, int max) {
+  int n = 0;
+  const char *s = p;
+  for (const char *q = p;; ++q) {
+    if (q == e || *q == '\t') {
+      if (n < max) {
+        fb[n] = s;
+        fe[n] = q;
+      }
+      ++n;
+      if (q == e) break;
+      s = q + 1;
+    }
+  }
+  return n;
+}
+
+bool parse_int(const char *b, const char *e, int64_t *out) {
+  if (b == e) return false;
+  bool neg = false;
+  if (*b == '-' || *b == '+') {
+    neg = *b == '-';
+    ++b;
+  }
+  if (b == e) return false;
+  int64_t v = 0;
+  for (; b < e; ++b) {
+    if (*b < '0' || *b > '9') return false;
+    v = v * 10 + (*b - '0');
+    if (v > (int64_t)1 << 53) return false;
+  }
+  *out = neg ? -v : v;
+  return true;
+}
+
+bool parse_value(const char *b, const char *e, double *out) {
+  int64_t iv;
+  if (parse_int(b, e, &iv)) {
+    *out = (double)iv;
+    return true;
+  }
+  std::string s(b, e);
+  char *end = nullptr;
+  errno = 0;
+  const double v = strtod(s.c_str(), &end);
+  if (end == s.c_str() || *end != '\0') return false;
+  *out = v;
+  return true;
+}
+
+/* Python 2 str(float): '%.12g', plus ".0" when the text has no '.', exponent or letter */
+int py2_float(char *buf, size_t cap, double x) {
+  if (std::isnan(x)) return snprintf(buf, cap, "nan");
+  if (std::isinf(x)) return snprintf(buf, cap, x > 0 ? "inf" : "-inf");
+  int n = snprintf(buf, cap, "%.12g", x);
+  if (!strpbrk(buf, ".e")) n += snprintf(buf + n, cap - n, ".0");
+  return n;
+}
+
+}  // namespace
+
+namespace {
+
+/* runs of consecutive lines with the same seqid, parsed from one chunk of the file */
+struct Run {
+  std::string seqid;
+  std::vector<int32_t> starts;
+  std::vector<double> vals;
+};
+
+struct Chunk {
+  std::vector<Run> runs;
+  bool ok = true;
+  std::string err;
+};
+
+/* parse the data lines of [p, end): '#' lines are comments (column headers are read
+ * up front, before the data) */
+void parse_chunk(const char *p, const char *end, const Columns &col, Chunk *out) {
+  Run *cur = nullptr;
+  while (p < end) {
+    const char *nl = (const char *)memchr(p, '\n', (size_t)(end - p));
+    const char *le = nl ? nl : end;
+    const char *line_end = (le > p && le[-1] == '\r') ? le - 1 : le;
+    if (line_end > p && p[0] != '#') {
+      const char *fb[32], *fe[32];
+      const int n = split_tabs(p, line_end, fb, fe, 32);
+      int64_t pos;
+      double val;
+      if (n <= col.seqid || n <= col.start || n <= col.value || !parse_int(fb[col.start], fe[col.start], &pos) ||
+          pos < INT32_MIN || pos > INT32_MAX || !parse_value(fb[col.value], fe[col.value], &val)) {
+        out->ok = false;
+        out->err = "malformed data line: " + std::string(p, (size_t)std::min<ptrdiff_t>(line_end - p, 80));
+        return;
+      }
+      const size_t nlen = (size_t)(fe[col.seqid] - fb[col.seqid]);
+      if (!cur || nlen != cur->seqid.size() || memcmp(fb[col.seqid], cur->seqid.data(), nlen) != 0) {
+        out->runs.emplace_back();
+        cur = &out->runs.back();
+        cur->seqid.assign(fb[col.seqid], nlen);
+      }
+      cur->starts.push_back((int32_t)pos);
+      cur->vals.push_back(val);
+    }
+    p = nl ? nl + 1 : end;
+  }
+}
+
+}  // namespace
+
+extern "C" gd_gtrack *gd_gtrack_read(const char *path) {
+  if (!path) {
+    gd_set_error("null path");
+    return nullptr;
+  }
+  const int fd = open(path, O_RDONLY);
+  if (fd < 0) {
+    gd_set_error((std::string("cannot open ") + path + ": " + strerror(errno)).c_str());
+    return nullptr;
+  }
+  struct stat st;
+  if (fstat(fd, &st) != 0) {
+    close(fd);
+    gd_set_error("fstat failed");
+    return nullptr;
+  }
+  const size_t size = (size_t)st.st_size;
+  const char *data = nullptr;
+  if (size > 0) {
+    void *m = mmap(nullptr, size, PROT_READ, MAP_PRIVATE, fd, 0);
+    if (m == MAP_FAILED) {
+      close(fd);
+      gd_set_error("mmap failed");
+      return nullptr;
+    }
+    madvise(m, size, MADV_SEQUENTIAL);
+    data = (const char *)m;
+  }
+  close(fd);
+
+  /* leading '#' lines: the "###" line names the columns */
+  Columns col;
+  const char *p = data, *end = data + size;
+  std::string err;
+  while (p < end && *p == '#') {
+    const char *nl = (const char *)memchr(p, '\n', (size_t)(end - p));
+    const char *le = nl ? nl : end;
+    const char *line_end = (le > p && le[-1] == '\r') ? le - 1 : le;
+    if (line_end - p > 3 && p[1] == '#' && p[2] == '#' && p[3] != '#') {
+      const char *fb[32], *fe[32];
+      const int n = split_tabs(p + 3, line_end, fb, fe, 32);
+      Columns c;
+      c.seqid = c.start = c.value = -1;
+      c.ncol = n;
+      for (int k = 0; k < n && k < 32; ++k) {
+        const std::string name(fb[k], fe[k]);
+        if (name == "seqid") c.seqid = k;
+        if (name == "start") c.start = k;
+        if (name == "value") c.value = k;
+      }
+      if (c.seqid < 0 || c.start < 0 || c.value < 0) err = "column header lacks seqid/start/value";
+      col = c;
+    }
+    p = nl ? nl + 1 : end;
+  }
+
+  /* data: chunks split at line boundaries, parsed in parallel, runs merged in order */
+  std::vector<Chunk> chunks;
+  if (err.empty() && p < end) {
+    const size_t bytes = (size_t)(end - p);
+    unsigned hw = std::thread::hardware_concurrency();
+    int T = (int)std::min<size_t>(std::max(1u, std::min(hw, 16u)), std::max<size_t>(1, bytes >> 24));
+    std::vector<const char *> cut(T + 1);
+    cut[0] = p;
+    cut[T] = end;
+    for (int k = 1; k < T; ++k) {
+      const char *q = p + bytes * k / T;
+      if (q < cut[k - 1]) q = cut[k - 1];
+      const char *nl = (const char *)memchr(q, '\n', (size_t)(end - q));
+      cut[k] = nl ? nl + 1 : end;
+    }
+    chunks.resize(T);
+    std::vector<std::thread> th;
+    for (int k = 1; k < T; ++k) th.emplace_back(parse_chunk, cut[k], cut[k + 1], std::cref(col), &chunks[k]);
+    parse_chunk(cut[0], cut[1], col, &chunks[0]);
+    for (auto &x : th) x.join();
+    for (auto &c : chunks)
+      if (!c.ok && err.empty()) err = c.err;
+  }
+  if (data) munmap((void *)data, size);
+  if (!err.empty()) {
+    gd_set_error((std::string(path) + ": " + err).c_str());
+    return nullptr;
+  }
+  gd_gtrack *t = new gd_gtrack();
+  std::unordered_map<std::string, int> index;
+  for (auto &c : chunks)
+    for (auto &r : c.runs) {
+      auto it = index.find(r.seqid);
+      int s;
+      if (it == index.end()) {
+        s = (int)t->seqid.size();
+        index.emplace(r.seqid, s);
+        t->seqid.push_back(r.seqid);
+        t->starts.emplace_back(std::move(r.starts));
+        t->vals.emplace_back(std::move(r.vals));
+        continue;
+      }
+      s = it->second;
+      t->starts[s].insert(t->starts[s].end(), r.starts.begin(), r.starts.end());
+      t->vals[s].insert(t->vals[s].end(), r.vals.begin(), r.vals.end());
+    }
+  return t;
+}
+
+extern "C" void gd_gtrack_free(gd_gtrack *t) { delete t; }
+
+extern "C" int gd_gtrack_nseq(const gd_gtrack *t) { return t ? (int)t->seqid.size() : 0; }
+
+extern "C" const char *gd_gtrack_seqid(const gd_gtrack *t, int s) {
+  return (t && s >= 0 && s < (int)t->seqid.size()) ? t->seqid[s].c_str() : nullptr;
+}
+
+extern "C" int64_t gd_gtrack_len(const gd_gtrack *t, int s) {
+  return (t && s >= 0 && s < (int)t->seqid.size()) ? (int64_t)t->starts[s].size() : -1;
+}
+
+extern "C" int gd_gtrack_copy(const gd_gtrack *t, int s, int32_t *starts, double *vals) {
+  if (!t || s < 0 || s >= (int)t->seqid.size()) {
+    gd_set_error("bad sequence index");
+    return GD_ERR_ARG;
+  }
+  const size_t n = t->starts[s].size();
+  if (starts && n) memcpy(starts, t->starts[s].data(), n * sizeof(int32_t));
+  if (vals && n) memcpy(vals, t->vals[s].data(), n * sizeof(double));
+  return GD_OK;
+}
+
+extern "C" int gd_write_tabular(const char *path, int append, const char *header, const char *seqid, int wstep,
+                                int64_t n, const double *scores, const double *other) {
+  if (!path || !seqid || wstep <= 0 || n < 0 || (n > 0 && (!scores || !other))) {
+    gd_set_error("bad tabular-writer arguments");
+    return GD_ERR_ARG;
+  }
+  FILE *f = fopen(path, append ? "ab" : "wb");
+  if (!f) {
+    gd_set_error((std::string("cannot open ") + path + ": " + strerror(errno)).c_str());
+    return GD_ERR_ARG;
+  }
+  std::vector<char> buf(1 << 20);
+  setvbuf(f, buf.data(), _IOFBF, buf.size());
+  if (header) fprintf(f, "%s\n", header);
+  char a[64], b[64];
+  for (int64_t i = 0; i < n; ++i) {
+    if (scores[i] == 0) continue; /* 0 and -0.0 mean "no window" (Q5) */
+    py2_float(a, sizeof a, scores[i]);
+    py2_float(b, sizeof b, other[i]);
+    fprintf(f, "%s\t%lld\t%s\t%s\n", seqid, (long long)(i * (int64_t)wstep), a, b);
+  }
+  const int bad = ferror(f);
+  if (fclose(f) != 0 || bad) {
+    gd_set_error("write failed");
+    return GD_ERR_ARG;
+  }
+  return GD_OK;
+}
+
+extern "C" int gd_format_py2_float(double x, char *buf, int cap) {
+  if (!buf || cap <= 0) return GD_ERR_ARG;
+  return py2_float(buf, (size_t)cap, x);
+}

@@ -29,9 +29,11 @@ EXPORTS = (
     "gd_fet_threadcompute", "gd_fet_compute", "gd_fet_scan_host",
     "gd_css_threadcompute", "gd_css_compute", "gd_css_scan_host",
     "gd_ctx_create", "gd_ctx_destroy", "gd_window_count",
-    "gd_fet_scan_device", "gd_css_scan_device",
+    "gd_fet_scan_device", "gd_css_scan_device", "gd_fet_scan_host_batch", "gd_css_scan_host_batch",
     "gd_set_seed", "gd_get_seed", "gd_last_error", "gd_device_count",
     "gd_last_stage_ms", "gd_synth_device",
+    "gd_gtrack_read", "gd_gtrack_free", "gd_gtrack_nseq", "gd_gtrack_seqid", "gd_gtrack_len", "gd_gtrack_copy",
+    "gd_write_tabular", "gd_format_py2_float",
 )
 
 
@@ -81,6 +83,24 @@ def _load() -> C.CDLL:
     lib.gd_last_error.restype = C.c_char_p
     lib.gd_last_stage_ms.argtypes = [C.POINTER(C.c_float), i32]
     lib.gd_synth_device.argtypes = [i32, i32, i32, i32, C.c_uint64, vp, vp, vp, vp, vp, vp]
+    lib.gd_fet_scan_host_batch.argtypes = [C.POINTER(Chrom), i32, dp, dp, ip, ip, i32, i32, C.c_double, i32, dp, dp]
+    lib.gd_css_scan_host_batch.argtypes = [C.POINTER(Chrom), i32, dp, dp, ip, ip, i32, i32, i32, i32, i32, dp, dp]
+    lib.gd_fet_scan_host_batch.restype = C.c_int
+    lib.gd_css_scan_host_batch.restype = C.c_int
+    lib.gd_gtrack_read.argtypes = [C.c_char_p]
+    lib.gd_gtrack_read.restype = vp
+    lib.gd_gtrack_free.argtypes = [vp]
+    lib.gd_gtrack_free.restype = None
+    lib.gd_gtrack_nseq.argtypes = [vp]
+    lib.gd_gtrack_seqid.argtypes = [vp, i32]
+    lib.gd_gtrack_seqid.restype = C.c_char_p
+    lib.gd_gtrack_len.argtypes = [vp, i32]
+    lib.gd_gtrack_len.restype = C.c_int64
+    lib.gd_gtrack_copy.argtypes = [vp, i32, vp, vp]
+    lib.gd_write_tabular.argtypes = [C.c_char_p, i32, C.c_char_p, C.c_char_p, i32, C.c_int64, vp, vp]
+    lib.gd_format_py2_float.argtypes = [C.c_double, C.c_char_p, i32]
+    for fn in ("gd_gtrack_nseq", "gd_gtrack_copy", "gd_write_tabular", "gd_format_py2_float"):
+        getattr(lib, fn).restype = C.c_int
     for fn in ("gd_fet_threadcompute", "gd_fet_compute", "gd_fet_scan_host", "gd_css_threadcompute",
                "gd_css_compute", "gd_css_scan_host", "gd_fet_scan_device", "gd_css_scan_device",
                "gd_synth_device", "gd_device_count", "gd_window_count", "gd_last_stage_ms"):

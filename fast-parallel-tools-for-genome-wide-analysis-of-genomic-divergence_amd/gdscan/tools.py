@@ -1,0 +1,79 @@
+"""End-to-end tools: two population GTrack files in, the HyperBrowser tools' tabular
+result out, every chromosome scanned in one device batch.
+
+fisher_exact_test_snp       <- tools/FisherExactTestSNPTool.py:140-189 (execute)
+cluster_separation_score    <- tools/ClusterSeparationScore.py:150-205 (execute)
+
+Differences from the Galaxy tools: chromosomes come in the order track A lists them
+(HyperBrowser iterates the genome's chromosome list); the region of a chromosome is
+[0, chrom_lengths[seqid]) when given, else [0, last position + 1) (HyperBrowser uses
+the genome build's chromosome length).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from ._lib import GD_WINDOWS_THREADED, Chrom, check, lib
+from .gtrack import read_gtrack, write_tabular
+
+
+def _batch(track_a, track_b, wstep, chrom_lengths):
+    ta, tb = read_gtrack(track_a), read_gtrack(track_b)
+    names = [s for s in ta if s in tb and len(ta[s][0]) > 0]
+    chroms = (Chrom * max(len(names), 1))()
+    av, bv, ap, bp = [], [], [], []
+    off_a = off_b = w = 0
+    for c, s in enumerate(names):
+        (pa, va), (pb, vb) = ta[s], tb[s]
+        regend = int(chrom_lengths[s]) if chrom_lengths and s in chrom_lengths else \
+            int(max(pa[-1], pb[-1] if len(pb) else 0)) + 1
+        chroms[c].a_off, chroms[c].b_off = off_a, off_b
+        chroms[c].alen, chroms[c].blen = len(va), len(vb)
+        chroms[c].regend, chroms[c].w_out = regend, w
+        chroms[c].seed = lib.gd_get_seed()
+        av.append(va); bv.append(vb); ap.append(pa); bp.append(pb)
+        off_a += len(va); off_b += len(vb); w += regend // wstep
+    cat = lambda xs, dt: np.ascontiguousarray(np.concatenate(xs) if xs else np.zeros(0), dtype=dt)
+    return names, chroms, cat(av, np.float64), cat(bv, np.float64), cat(ap, np.int32), cat(bp, np.int32), w
+
+
+def _write(out_path, header, names, chroms, wstep, s0, s1):
+    write_tabular(out_path, names[0] if names else "", wstep, np.zeros(0), np.zeros(0), header=header, append=False)
+    for c, s in enumerate(names):
+        lo = chroms[c].w_out
+        n = chroms[c].regend // wstep
+        write_tabular(out_path, s, wstep, s0[lo:lo + n], s1[lo:lo + n])
+
+
+def _ptr(a, ct):
+    import ctypes as C
+    return a.ctypes.data_as(C.POINTER(ct))
+
+
+def fisher_exact_test_snp(track_a, track_b, out_path, wsize=2500, wstep=500, percentile=0.95, chrom_lengths=None):
+    import ctypes as C
+    names, chroms, av, bv, ap, bp, w = _batch(track_a, track_b, wstep, chrom_lengths)
+    scores, stddev = np.zeros(w), np.zeros(w)
+    if names:
+        check(lib.gd_fet_scan_host_batch(chroms, len(names), _ptr(av, C.c_double), _ptr(bv, C.c_double),
+                                         _ptr(ap, C.c_int), _ptr(bp, C.c_int), int(wsize), int(wstep),
+                                         float(percentile), GD_WINDOWS_THREADED, _ptr(scores, C.c_double),
+                                         _ptr(stddev, C.c_double)))
+    _write(out_path, "#seqid\tstart\tscore\tstddev", names, chroms, wstep, scores, stddev)
+    return names, scores, stddev
+
+
+def cluster_separation_score(track_a, track_b, out_path, wsize=2500, wstep=500, mc_treshold=10, mc_runs=0,
+                             compare="count", mds="classical", chrom_lengths=None):
+    import ctypes as C
+    if compare != "count" or mds != "classical":
+        raise ValueError("only the count metric with classical MDS is implemented (DESIGN.md section 6)")
+    names, chroms, av, bv, ap, bp, w = _batch(track_a, track_b, wstep, chrom_lengths)
+    scores, p = np.zeros(w), np.zeros(w)
+    if names:
+        check(lib.gd_css_scan_host_batch(chroms, len(names), _ptr(av, C.c_double), _ptr(bv, C.c_double),
+                                         _ptr(ap, C.c_int), _ptr(bp, C.c_int), int(wsize), int(wstep),
+                                         int(mc_treshold), int(mc_runs), GD_WINDOWS_THREADED,
+                                         _ptr(scores, C.c_double), _ptr(p, C.c_double)))
+    _write(out_path, "#seqid\tstart\tscore\tp", names, chroms, wstep, scores, p)
+    return names, scores, p

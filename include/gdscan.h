@@ -96,6 +96,15 @@ int gd_css_scan_device(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, const do
                        const int32_t *apos, const int32_t *bpos, int wsize, int wstep, int treshold, int runs,
                        int window_set, double *scores, double *p, void *hip_stream);
 
+/* the same batch from host memory (offsets into host arrays; outputs are caller-owned
+ * host arrays holding every chromosome's w_out + regend/wstep windows) */
+int gd_fet_scan_host_batch(const gd_chrom *chroms, int nchrom, const double *avals, const double *bvals,
+                           const int *apos, const int *bpos, int wsize, int wstep, double perc, int window_set,
+                           double *scores, double *stddev);
+int gd_css_scan_host_batch(const gd_chrom *chroms, int nchrom, const double *avals, const double *bvals,
+                           const int *apos, const int *bpos, int wsize, int wstep, int treshold, int runs,
+                           int window_set, double *scores, double *p);
+
 /* ---- configuration / diagnostics ---- */
 void gd_set_seed(uint64_t seed);     /* seed used by the reference-signature entry points */
 uint64_t gd_get_seed(void);
@@ -118,6 +127,21 @@ int gd_last_stage_ms(float *ms, int n);
 /* ---- synthetic tracks generated on the device (identical to gdscan/synth.py) ---- */
 int gd_synth_device(int chrom, int nsnp, int asize, int bsize, uint64_t seed, const double *freq_table,
                     double *avals, double *bvals, int32_t *apos, int32_t *bpos, void *hip_stream);
+
+/* ---- HyperBrowser track I/O: GTrack "valued points" reader and the
+ * tools' tabular writer (FisherExactTestSNPTool.py:162-189, ClusterSeparationScore.py:180-205) ---- */
+typedef struct gd_gtrack gd_gtrack;
+gd_gtrack *gd_gtrack_read(const char *path); /* NULL on failure (gd_last_error) */
+void gd_gtrack_free(gd_gtrack *t);
+int gd_gtrack_nseq(const gd_gtrack *t);                   /* sequences, in first-seen order */
+const char *gd_gtrack_seqid(const gd_gtrack *t, int s);
+int64_t gd_gtrack_len(const gd_gtrack *t, int s);         /* elements of sequence s */
+int gd_gtrack_copy(const gd_gtrack *t, int s, int32_t *starts, double *vals);
+/* appends (or creates) `path`: optional header line, then one line per window with
+ * scores[i] != 0: "seqid\t<i*wstep>\t<score>\t<other>", floats as Python 2 str() */
+int gd_write_tabular(const char *path, int append, const char *header, const char *seqid, int wstep, int64_t n,
+                     const double *scores, const double *other);
+int gd_format_py2_float(double x, char *buf, int cap); /* returns the text length */
 
 #ifdef __cplusplus
 }
