@@ -159,3 +159,48 @@ def test_popcount_path_equals_literal_path_full_chromosome(monkeypatch):
     monkeypatch.delenv("GD_CSS_FORCE_LITERAL")
     assert np.array_equal(s_fast, s_lit, equal_nan=True)
     assert (s_fast != 0).sum() > 45_000
+
+
+def _dense(av, bv, ap, bp, a, b, step):
+    """Re-space the SNPs every `step` bp (denser windows: more than 64 SNPs each)."""
+    rows = len(ap) // a
+    pos = (np.arange(rows, dtype=np.int32) + 1) * step
+    return av, bv, np.repeat(pos, a), np.repeat(pos, b), int(pos[-1]) + 1
+
+
+def test_dense_windows_multi_chunk(oracle):
+    """Windows of ~250 SNPs: the popcount build runs 4 64-SNP chunks per window."""
+    from gdscan import css
+    av, bv, ap, bp, _ = _synth(12, 6_000, 8, 8)
+    av, bv, ap, bp, regend = _dense(av, bv, ap, bp, 8, 8, 10)
+    s, p = css.scan(av, bv, ap, bp, regend, treshold=5, runs=40, seed=3)
+    s_ref, p_ref = oracle_css_scan(oracle, av, bv, ap, bp, regend, treshold=5, runs=40, seed=3)
+    _cmp_scores(s, s_ref)
+    assert (p == p_ref).mean() >= 0.99
+
+
+def test_largest_tier_64_plus_64(oracle):
+    from gdscan import css
+    av, bv, ap, bp, regend = _synth(13, 1_800, 64, 64)
+    s, p = css.scan(av, bv, ap, bp, regend)
+    s_ref, p_ref = oracle_css_scan(oracle, av, bv, ap, bp, regend)
+    _cmp_scores(s, s_ref)
+
+
+def test_empty_population_writes_nothing():
+    from gdscan import css
+    av, bv, ap, bp, regend = _synth(14, 3_000, 4, 4)
+    import css_cython_parallel as ccp
+    out_s, out_p = np.full(regend // 500, 7.0), np.full(regend // 500, 7.0)
+    ccp.cluster_separation_scorer(av, bv[:0], ap, bp[:0], 0, regend, 2500, 500, len(av), 0, 10, 0, 0, 0, out_s,
+                                  out_p)
+    assert np.all(out_s == 7.0) and np.all(out_p == 7.0)
+
+
+def test_serial_window_set_with_permutations(oracle):
+    from gdscan import css
+    av, bv, ap, bp, regend = _synth(15, 12_000, 9, 11)
+    s, p = css.scan(av, bv, ap, bp, regend, treshold=10, runs=200, seed=9, serial=True)
+    s_ref, p_ref = oracle_css_scan(oracle, av, bv, ap, bp, regend, treshold=10, runs=200, seed=9, serial=True)
+    _cmp_scores(s, s_ref)
+    assert (p[s_ref != 0] == p_ref[s_ref != 0]).mean() >= 0.995

@@ -241,3 +241,28 @@ def test_rejected_draws_are_redrawn(oracle):
     s, d = fet.scan(av, bv, ap, bp, regend, wsize, wstep, perc, seed=seed)
     assert close(s, s_ref) and close(d, d_ref)
     assert close(d[hit], d_ref[hit])
+
+
+def test_empty_population_writes_nothing():
+    """alen or blen == 0: the reference computes nothing; outputs keep the caller's values."""
+    import fisher_cython_parallel as fcp
+    av, bv, ap, bp, regend = _synth(30, 3000, 4, 4)
+    for a_cut, b_cut in ((0, len(bv)), (len(av), 0)):
+        s, d = np.full(regend // 500, 7.0), np.full(regend // 500, 7.0)
+        fcp.fisher_exact_tester(av[:a_cut], bv[:b_cut], ap[:a_cut], bp[:b_cut], 0, regend, 2500, 500, a_cut, b_cut,
+                                0.95, s, d)
+        assert np.all(s == 7.0) and np.all(d == 7.0)
+
+
+def test_mid_size_windows_counting_rank(oracle):
+    """64 < n <= 256 SNPs per window: the fast path's counting ranks."""
+    from gdscan import fet
+    av, bv, ap, bp, regend = _synth(31, 20000, 6, 6)
+    rows = len(ap) // 6
+    pos = (np.arange(rows, dtype=np.int32) + 1) * 20  # ~125 SNPs per 2.5 kb window
+    ap, bp = np.repeat(pos, 6), np.repeat(pos, 6)
+    regend = int(pos[-1]) + 1
+    s, d = fet.scan(av, bv, ap, bp, regend, seed=5)
+    s_ref, d_ref = oracle_fet_scan(oracle, av, bv, ap, bp, regend, seed=5)
+    assert (s_ref != 0).sum() > 500
+    assert close(s, s_ref) and close(d, d_ref)
