@@ -54,10 +54,9 @@ __device__ unsigned long long g_css_prof[8];
 #define CSS_PROF(ph)
 #endif
 
-/* waves per SIMD the register allocator must reach for k_css_mds<MP>: the kernel is
- * latency-bound, so occupancy beats the few cold spills it costs (MP=40: 4 waves,
- * 12 VGPRs spilled, 9 % faster than the unconstrained 3 waves) */
-#define CSS_MDS_WAVES(MP) ((MP) <= 24 ? 5 : (MP) <= 40 ? 4 : (MP) <= 64 ? 2 : (MP) <= 96 ? 3 : 2)
+/* waves per SIMD the register allocator must reach for k_css_mds<MP> (measured per
+ * tier: the compile-time-K steps of MP <= 40 run best at 3-4 waves without spills) */
+#define CSS_MDS_WAVES(MP) ((MP) <= 24 ? 4 : (MP) <= 40 ? 3 : (MP) <= 64 ? 2 : (MP) <= 96 ? 3 : 2)
 
 namespace {
 
@@ -307,6 +306,98 @@ __device__ __forceinline__ double pair_sum(double x) {
     return x + dpp64<0xB1, 0xF>(x, 0.0); /* quad_perm [1,0,3,2]: the partner lane */
 }
 
+/* One Householder step with the column index K known at compile time (single-wave
+ * tiers up to 40 individuals): block skipping, the dead-column stash and the reads
+ * of x, d_K and A e_{K+1} all resolve to fixed registers -- no per-column selects. */
+template <int MP, int K>
+__device__ __forceinline__ void hh_step_static(double (&A)[MP], int m, int i, int ii, int tid, bool row,
+                                               double *s_row, double *s_v, double *s_w, double *s_d, double *s_e,
+                                               double *s_tau, double *s_red) {
+  __syncthreads();
+  if (i == K) {
+#pragma unroll
+    for (int jb = 0; jb < MP / 8; ++jb)
+      if (8 * jb + 7 >= K) {
+#pragma unroll
+        for (int u = 0; u < 8; u += 2) {
+          const int j = 8 * jb + u;
+          *reinterpret_cast<double2 *>(s_row + j) = make_double2(j > K ? A[j] : 0.0, j + 1 > K ? A[j + 1] : 0.0);
+        }
+      }
+    s_d[K] = A[K];
+  }
+  __syncthreads();
+  if (K >= m - 2) {
+    if (tid == 0 && K == m - 2) s_e[K] = s_row[K + 1];
+    return;
+  }
+  const double xi = (i > K + 1 && row) ? s_row[ii] : 0.0;
+  const double alpha = s_row[K + 1];
+  double p0 = 0, p1 = 0;
+#pragma unroll
+  for (int jb = 0; jb < MP / 8; ++jb) {
+    if (8 * jb + 7 > K) {
+#pragma unroll
+      for (int u = 0; u < 8; u += 2) {
+        if (8 * jb + u > K) p0 = fma(A[8 * jb + u], s_row[8 * jb + u], p0);
+        if (8 * jb + u + 1 > K) p1 = fma(A[8 * jb + u + 1], s_row[8 * jb + u + 1], p1);
+      }
+      CSS_PIN(p0);
+      CSS_PIN(p1);
+    }
+  }
+  const double ak1 = A[K + 1];
+  const double sigma = block_sum<1>(xi * xi, s_red);
+  double tau = 0.0, beta = alpha, scale = 0.0;
+  if (sigma != 0.0) {
+    beta = -copysign(sqrt(alpha * alpha + sigma), alpha);
+    tau = (beta - alpha) * fast_rcp(beta);
+    scale = fast_rcp(alpha - beta);
+  }
+  const double vi = (i == K + 1) ? 1.0 : xi * scale;
+  const double pi = (i > K && row) ? (tau * scale) * fma(-beta, ak1, p0 + p1) : 0.0;
+  const double Kc = -0.5 * tau * block_sum<1>(pi * vi, s_red);
+  const double wi = fma(Kc, vi, pi);
+  if (tid == 0) {
+    s_e[K] = beta;
+    s_tau[K] = tau;
+  }
+  if (i < MP) {
+    s_v[i] = vi;
+    s_w[i] = wi;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int jb = 0; jb < MP / 8; ++jb) {
+    if (8 * jb + 7 > K) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int j = 8 * jb + u;
+        if (j > K) A[j] = fma(-vi, s_w[j], fma(-wi, s_v[j], A[j]));
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) CSS_PIN(A[8 * jb + u]);
+    }
+  }
+  A[K] = vi; /* stash v_K in the dead column K */
+}
+
+template <int MP, int K>
+struct HhStatic {
+  static __device__ __forceinline__ void run(double (&A)[MP], int m, int i, int ii, int tid, bool row, double *s_row,
+                                             double *s_v, double *s_w, double *s_d, double *s_e, double *s_tau,
+                                             double *s_red) {
+    if (K >= m) return;
+    hh_step_static<MP, K>(A, m, i, ii, tid, row, s_row, s_v, s_w, s_d, s_e, s_tau, s_red);
+    HhStatic<MP, K + 1>::run(A, m, i, ii, tid, row, s_row, s_v, s_w, s_d, s_e, s_tau, s_red);
+  }
+};
+template <int MP>
+struct HhStatic<MP, MP> {
+  static __device__ __forceinline__ void run(double (&)[MP], int, int, int, int, bool, double *, double *, double *,
+                                             double *, double *, double *, double *) {}
+};
+
 template <int MP, int G>
 __global__ void __launch_bounds__((CssShape<MP, G>::NT), CSS_MDS_WAVES(MP))
     k_css_mds(const gd_chrom_dev *ch, int nchrom, const gd_css_planes *pl, const uint32_t *planes,
@@ -510,6 +601,9 @@ __global__ void __launch_bounds__((CssShape<MP, G>::NT), CSS_MDS_WAVES(MP))
      * of each row holds that row's element of the reflector v_k.  Columns are
      * handled in blocks of 8; a block dead in every column part (v, w and x are 0
      * left of k) is skipped by a uniform branch. */
+    if constexpr (G == 1 && MP <= 40) {
+      HhStatic<MP, 0>::run(A, m, i, ii, tid, row, s_row, s_v, s_w, s_d, s_e, s_tau, s_red);
+    } else
     for (int k = 0; k < m; ++k) {
       __syncthreads();
       /* row k's lanes publish x = row k right of the diagonal (zeros at j <= k) and d_k */
