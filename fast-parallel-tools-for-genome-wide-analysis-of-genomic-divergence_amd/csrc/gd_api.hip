@@ -755,3 +755,49 @@ extern "C" int gd_synth_device(int chrom, int nsnp, int asize, int bsize, uint64
   return gd_synth_launch(chrom, nsnp, asize, bsize, seed, freq_table, avals, bvals, apos, bpos,
                          (hipStream_t)hip_stream);
 }
+
+/* ------------------------------------------------- region filters (gd_regions.hip) */
+int gd_rg_fet_limit(const double *scores, const double *stddev, int64_t n, double qnorm, double percentile,
+                    double *out, hipStream_t s);
+int gd_rg_fdr_threshold(const double *p, int64_t n, double fdr, double *testp, int64_t *k_out, hipStream_t s);
+int gd_rg_top_limit(const double *scores, int64_t n, int64_t num_top, double *limit, hipStream_t s);
+int gd_rg_merge(const double *vals, const int32_t *seq, const int64_t *start, int64_t n, int cmp, double thr,
+                int64_t gap, const int64_t *seq_end, int nseq, int64_t *region_first, int64_t *region_end,
+                int64_t *nregions, int64_t *nselected, hipStream_t s);
+
+/* ctx == NULL: the calling thread's default context (device 0); stream NULL: the context's */
+template <class F>
+static int with_ctx(gd_ctx *ctx, void *hip_stream, F &&f) {
+  int st = GD_OK;
+  if (!ctx) ctx = default_ctx(&st);
+  if (!ctx) return st ? st : fail(GD_ERR_HIP, "no device context");
+  std::lock_guard<std::mutex> g(ctx->mu);
+  HIP_TRY(hipSetDevice(ctx->device));
+  return f(hip_stream ? (hipStream_t)hip_stream : ctx->stream);
+}
+
+extern "C" int gd_fet_region_limit(gd_ctx *ctx, const double *scores, const double *stddev, int64_t n,
+                                   double qnorm, double percentile, double *out3, void *hip_stream) {
+  return with_ctx(ctx, hip_stream,
+                  [&](hipStream_t s) { return gd_rg_fet_limit(scores, stddev, n, qnorm, percentile, out3, s); });
+}
+
+extern "C" int gd_css_fdr_threshold(gd_ctx *ctx, const double *p, int64_t n, double fdr, double *testp,
+                                    int64_t *k, void *hip_stream) {
+  return with_ctx(ctx, hip_stream, [&](hipStream_t s) { return gd_rg_fdr_threshold(p, n, fdr, testp, k, s); });
+}
+
+extern "C" int gd_css_top_limit(gd_ctx *ctx, const double *scores, int64_t n, int64_t num_top, double *limit,
+                                void *hip_stream) {
+  return with_ctx(ctx, hip_stream, [&](hipStream_t s) { return gd_rg_top_limit(scores, n, num_top, limit, s); });
+}
+
+extern "C" int gd_merge_regions(gd_ctx *ctx, const double *vals, const int32_t *seq, const int64_t *start,
+                                int64_t n, int cmp, double thr, int64_t max_gap, const int64_t *seq_end, int nseq,
+                                int64_t *region_first, int64_t *region_end, int64_t *nregions, int64_t *nselected,
+                                void *hip_stream) {
+  return with_ctx(ctx, hip_stream, [&](hipStream_t s) {
+    return gd_rg_merge(vals, seq, start, n, cmp, thr, max_gap, seq_end, nseq, region_first, region_end, nregions,
+                       nselected, s);
+  });
+}

@@ -346,7 +346,7 @@ __device__ __forceinline__ void hh_step_static(double (&A)[MP], int m, int i, in
       CSS_PIN(p1);
     }
   }
-  const double ak1 = A[K + 1];
+  const double ak1 = A[K + 1 < MP ? K + 1 : K]; /* K >= MP - 2 returned above */
   const double sigma = block_sum<1>(xi * xi, s_red);
   double tau = 0.0, beta = alpha, scale = 0.0;
   if (sigma != 0.0) {

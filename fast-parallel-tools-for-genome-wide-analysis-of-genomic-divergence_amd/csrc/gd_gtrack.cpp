@@ -321,3 +321,181 @@ extern "C" int gd_format_py2_float(double x, char *buf, int cap) {
   if (!buf || cap <= 0) return GD_ERR_ARG;
   return py2_float(buf, (size_t)cap, x);
 }
+
+/* ------------------------------------------------------------------------------------
+ * Tabular reader for the region filters: the tools' result files as
+ * FilterFisherScores.preProcessPvalues / SignificantCSSRegions.preProcessPvalues read
+ * them (FilterFisherScores.py:117-131, SignificantCSSRegions.py:157-173): every line
+ * that is non-empty and does not start with '#' is "seqid \t start \t col2 \t col3 ...";
+ * the address is (seqid, start), col2/col3 parse like Python float().  A line with
+ * fewer than four fields is an error (the tools raise IndexError).  The start must be
+ * an integer (the merge calls int() on it); it is kept as int64 and written back in
+ * canonical decimal.
+ */
+struct gd_tabular {
+  std::vector<std::string> seqid;
+  std::vector<int32_t> seq;
+  std::vector<int64_t> start;
+  std::vector<double> c2, c3;
+};
+
+namespace {
+
+struct TabChunk {
+  std::vector<std::string> names; /* chunk-local first-seen order */
+  std::vector<int32_t> seq;
+  std::vector<int64_t> start;
+  std::vector<double> c2, c3;
+  bool ok = true;
+  std::string err;
+};
+
+void parse_tab_chunk(const char *p, const char *end, TabChunk *out) {
+  int cur = -1;
+  std::unordered_map<std::string, int> local;
+  while (p < end) {
+    const char *nl = (const char *)memchr(p, '\n', (size_t)(end - p));
+    const char *le = nl ? nl : end;
+    const char *line_end = (le > p && le[-1] == '\r') ? le - 1 : le;
+    if (le > p && p[0] != '#') {
+      const char *fb[4], *fe[4];
+      const int n = split_tabs(p, line_end, fb, fe, 4);
+      int64_t pos;
+      double a, b;
+      if (n < 4 || !parse_int(fb[1], fe[1], &pos) || !parse_value(fb[2], fe[2], &a) ||
+          !parse_value(fb[3], fe[3], &b)) {
+        out->ok = false;
+        out->err = "malformed result line: " + std::string(p, (size_t)std::min<ptrdiff_t>(line_end - p, 80));
+        return;
+      }
+      const size_t nlen = (size_t)(fe[0] - fb[0]);
+      if (cur < 0 || nlen != out->names[cur].size() || memcmp(fb[0], out->names[cur].data(), nlen) != 0) {
+        std::string name(fb[0], nlen);
+        auto it = local.find(name);
+        if (it == local.end()) {
+          cur = (int)out->names.size();
+          local.emplace(name, cur);
+          out->names.push_back(std::move(name));
+        } else {
+          cur = it->second;
+        }
+      }
+      out->seq.push_back(cur);
+      out->start.push_back(pos);
+      out->c2.push_back(a);
+      out->c3.push_back(b);
+    }
+    p = nl ? nl + 1 : end;
+  }
+}
+
+}  // namespace
+
+extern "C" gd_tabular *gd_tabular_read(const char *path) {
+  if (!path) {
+    gd_set_error("null path");
+    return nullptr;
+  }
+  const int fd = open(path, O_RDONLY);
+  if (fd < 0) {
+    gd_set_error((std::string("cannot open ") + path + ": " + strerror(errno)).c_str());
+    return nullptr;
+  }
+  struct stat st;
+  if (fstat(fd, &st) != 0) {
+    close(fd);
+    gd_set_error("fstat failed");
+    return nullptr;
+  }
+  const size_t size = (size_t)st.st_size;
+  const char *data = nullptr;
+  if (size > 0) {
+    void *m = mmap(nullptr, size, PROT_READ, MAP_PRIVATE, fd, 0);
+    if (m == MAP_FAILED) {
+      close(fd);
+      gd_set_error("mmap failed");
+      return nullptr;
+    }
+    madvise(m, size, MADV_SEQUENTIAL);
+    data = (const char *)m;
+  }
+  close(fd);
+  std::vector<TabChunk> chunks;
+  std::string err;
+  if (size > 0) {
+    const char *p = data, *end = data + size;
+    unsigned hw = std::thread::hardware_concurrency();
+    int T = (int)std::min<size_t>(std::max(1u, std::min(hw, 16u)), std::max<size_t>(1, size >> 24));
+    std::vector<const char *> cut(T + 1);
+    cut[0] = p;
+    cut[T] = end;
+    for (int k = 1; k < T; ++k) {
+      const char *q = p + size * k / T;
+      if (q < cut[k - 1]) q = cut[k - 1];
+      const char *nl = (const char *)memchr(q, '\n', (size_t)(end - q));
+      cut[k] = nl ? nl + 1 : end;
+    }
+    chunks.resize(T);
+    std::vector<std::thread> th;
+    for (int k = 1; k < T; ++k) th.emplace_back(parse_tab_chunk, cut[k], cut[k + 1], &chunks[k]);
+    parse_tab_chunk(cut[0], cut[1], &chunks[0]);
+    for (auto &x : th) x.join();
+    for (auto &c : chunks)
+      if (!c.ok && err.empty()) err = c.err;
+    munmap((void *)data, size);
+  }
+  if (!err.empty()) {
+    gd_set_error((std::string(path) + ": " + err).c_str());
+    return nullptr;
+  }
+  gd_tabular *t = new gd_tabular();
+  std::unordered_map<std::string, int> index;
+  size_t rows = 0;
+  for (auto &c : chunks) rows += c.seq.size();
+  t->seq.reserve(rows);
+  t->start.reserve(rows);
+  t->c2.reserve(rows);
+  t->c3.reserve(rows);
+  for (auto &c : chunks) {
+    std::vector<int32_t> glob(c.names.size());
+    for (size_t k = 0; k < c.names.size(); ++k) {
+      auto it = index.find(c.names[k]);
+      if (it == index.end()) {
+        glob[k] = (int32_t)t->seqid.size();
+        index.emplace(c.names[k], glob[k]);
+        t->seqid.push_back(c.names[k]);
+      } else {
+        glob[k] = it->second;
+      }
+    }
+    for (int32_t s : c.seq) t->seq.push_back(glob[s]);
+    t->start.insert(t->start.end(), c.start.begin(), c.start.end());
+    t->c2.insert(t->c2.end(), c.c2.begin(), c.c2.end());
+    t->c3.insert(t->c3.end(), c.c3.begin(), c.c3.end());
+  }
+  return t;
+}
+
+extern "C" void gd_tabular_free(gd_tabular *t) { delete t; }
+
+extern "C" int64_t gd_tabular_rows(const gd_tabular *t) { return t ? (int64_t)t->seq.size() : 0; }
+
+extern "C" int gd_tabular_nseq(const gd_tabular *t) { return t ? (int)t->seqid.size() : 0; }
+
+extern "C" const char *gd_tabular_seqid(const gd_tabular *t, int s) {
+  return (t && s >= 0 && s < (int)t->seqid.size()) ? t->seqid[s].c_str() : nullptr;
+}
+
+extern "C" int gd_tabular_copy(const gd_tabular *t, int32_t *seq, int64_t *start, double *col2, double *col3) {
+  if (!t) {
+    gd_set_error("null table");
+    return GD_ERR_ARG;
+  }
+  const size_t n = t->seq.size();
+  if (!n) return GD_OK;
+  if (seq) memcpy(seq, t->seq.data(), n * sizeof(int32_t));
+  if (start) memcpy(start, t->start.data(), n * sizeof(int64_t));
+  if (col2) memcpy(col2, t->c2.data(), n * sizeof(double));
+  if (col3) memcpy(col3, t->c3.data(), n * sizeof(double));
+  return GD_OK;
+}

@@ -23,6 +23,8 @@ GD_DEFAULT_SEED = 20261015
 GD_WINDOWS_THREADED = 0
 GD_WINDOWS_SERIAL = 1
 GD_NSTAGES = 4
+GD_SELECT_GE = 0
+GD_SELECT_LE = 1
 
 # every symbol include/gdscan.h declares
 EXPORTS = (
@@ -34,6 +36,9 @@ EXPORTS = (
     "gd_last_stage_ms", "gd_synth_device",
     "gd_gtrack_read", "gd_gtrack_free", "gd_gtrack_nseq", "gd_gtrack_seqid", "gd_gtrack_len", "gd_gtrack_copy",
     "gd_write_tabular", "gd_format_py2_float",
+    "gd_tabular_read", "gd_tabular_free", "gd_tabular_rows", "gd_tabular_nseq", "gd_tabular_seqid",
+    "gd_tabular_copy",
+    "gd_fet_region_limit", "gd_css_fdr_threshold", "gd_css_top_limit", "gd_merge_regions",
 )
 
 
@@ -99,6 +104,24 @@ def _load() -> C.CDLL:
     lib.gd_gtrack_copy.argtypes = [vp, i32, vp, vp]
     lib.gd_write_tabular.argtypes = [C.c_char_p, i32, C.c_char_p, C.c_char_p, i32, C.c_int64, vp, vp]
     lib.gd_format_py2_float.argtypes = [C.c_double, C.c_char_p, i32]
+    i64, pi64 = C.c_int64, C.POINTER(C.c_int64)
+    lib.gd_tabular_read.argtypes = [C.c_char_p]
+    lib.gd_tabular_read.restype = vp
+    lib.gd_tabular_free.argtypes = [vp]
+    lib.gd_tabular_free.restype = None
+    lib.gd_tabular_rows.argtypes = [vp]
+    lib.gd_tabular_rows.restype = i64
+    lib.gd_tabular_nseq.argtypes = [vp]
+    lib.gd_tabular_seqid.argtypes = [vp, i32]
+    lib.gd_tabular_seqid.restype = C.c_char_p
+    lib.gd_tabular_copy.argtypes = [vp, vp, vp, vp, vp]
+    lib.gd_fet_region_limit.argtypes = [vp, vp, vp, i64, C.c_double, C.c_double, dp, vp]
+    lib.gd_css_fdr_threshold.argtypes = [vp, vp, i64, C.c_double, dp, pi64, vp]
+    lib.gd_css_top_limit.argtypes = [vp, vp, i64, i64, dp, vp]
+    lib.gd_merge_regions.argtypes = [vp, vp, vp, vp, i64, i32, C.c_double, i64, vp, i32, vp, vp, pi64, pi64, vp]
+    for fn in ("gd_tabular_nseq", "gd_tabular_copy", "gd_fet_region_limit", "gd_css_fdr_threshold",
+               "gd_css_top_limit", "gd_merge_regions"):
+        getattr(lib, fn).restype = C.c_int
     for fn in ("gd_gtrack_nseq", "gd_gtrack_copy", "gd_write_tabular", "gd_format_py2_float"):
         getattr(lib, fn).restype = C.c_int
     for fn in ("gd_fet_threadcompute", "gd_fet_compute", "gd_fet_scan_host", "gd_css_threadcompute",

@@ -105,6 +105,34 @@ int gd_css_scan_host_batch(const gd_chrom *chroms, int nchrom, const double *ava
                            const int *apos, const int *bpos, int wsize, int wstep, int treshold, int runs,
                            int window_set, double *scores, double *p);
 
+/* ---- region filters after the scan ----
+ * A track is the list of windows a tool's tabular file holds (score != 0), in file
+ * order.  Array arguments may be host or device memory; ctx NULL selects the calling
+ * thread's default context, hip_stream NULL the context's stream.  Blocking. */
+#define GD_SELECT_GE 0 /* keep vals >= thr (FET scores, CSS top-k scores) */
+#define GD_SELECT_LE 1 /* keep vals <= thr (CSS p-values) */
+/* FilterFisherScores.py:84-87: out3 = {limit, cmedian(scores), scoreatpercentile(stddev,
+ * percentile)}, limit = median + qnorm * upperquant; qnorm = norm.ppf(normquantile) is the
+ * caller's (scipy.special.ndtri).  Non-finite scores: GD_ERR_ARG (numpy.histogram raises). */
+int gd_fet_region_limit(gd_ctx *ctx, const double *scores, const double *stddev, int64_t n, double qnorm,
+                        double percentile, double *out3, void *hip_stream);
+/* SignificantCSSRegions.py:102-120: Benjamini-Hochberg p threshold; *k = 0 ("NONE found")
+ * when no p passes */
+int gd_css_fdr_threshold(gd_ctx *ctx, const double *p, int64_t n, double fdr, double *testp, int64_t *k,
+                         void *hip_stream);
+/* SignificantCSSRegions.py:125-126: scores[argsort(scores)[::-1][num_top - 1]] (NaN ranks
+ * first, Python indexing; out of range: GD_ERR_ARG) */
+int gd_css_top_limit(gd_ctx *ctx, const double *scores, int64_t n, int64_t num_top, double *limit,
+                     void *hip_stream);
+/* FilterFisherScores.py:92-114 / SignificantCSSRegions.py:123-150: keep the windows passing
+ * `cmp thr` and merge them into segments: a segment breaks where the sequence changes or
+ * start - max_gap > previous kept start; it is written as (index of its first window,
+ * min(last start + max_gap, seq_end[seq])), seq_end = chromosome length - 1.  region_first
+ * / region_end need room for *nselected entries (n is always enough). */
+int gd_merge_regions(gd_ctx *ctx, const double *vals, const int32_t *seq, const int64_t *start, int64_t n, int cmp,
+                     double thr, int64_t max_gap, const int64_t *seq_end, int nseq, int64_t *region_first,
+                     int64_t *region_end, int64_t *nregions, int64_t *nselected, void *hip_stream);
+
 /* ---- configuration / diagnostics ---- */
 void gd_set_seed(uint64_t seed);     /* seed used by the reference-signature entry points */
 uint64_t gd_get_seed(void);
@@ -142,6 +170,15 @@ int gd_gtrack_copy(const gd_gtrack *t, int s, int32_t *starts, double *vals);
 int gd_write_tabular(const char *path, int append, const char *header, const char *seqid, int wstep, int64_t n,
                      const double *scores, const double *other);
 int gd_format_py2_float(double x, char *buf, int cap); /* returns the text length */
+/* the tools' result files read back for the region filters (FilterFisherScores.py:117-131,
+ * SignificantCSSRegions.py:157-173): rows "seqid\tstart\tcol2\tcol3", '#' lines skipped */
+typedef struct gd_tabular gd_tabular;
+gd_tabular *gd_tabular_read(const char *path); /* NULL on failure (gd_last_error) */
+void gd_tabular_free(gd_tabular *t);
+int64_t gd_tabular_rows(const gd_tabular *t);
+int gd_tabular_nseq(const gd_tabular *t);          /* seqids in first-seen order */
+const char *gd_tabular_seqid(const gd_tabular *t, int s);
+int gd_tabular_copy(const gd_tabular *t, int32_t *seq, int64_t *start, double *col2, double *col3);
 
 #ifdef __cplusplus
 }
