@@ -194,6 +194,54 @@ def cpu_baseline(args):
     }
 
 
+def regions_run(args, scores, stddev, chroms, nch, rank, world, dev):
+    """FilterFisherScores on the FET track just computed, kept in HBM:
+    the tabular track (windows with score != 0), its limit (cmedian + scoreatpercentile)
+    and the merged segments.  Timed end to end per call (host sync included)."""
+    import torch
+    from gdscan._lib import GD_SELECT_GE
+    from gdscan.regions import fet_region_limit, merge_regions
+    wcount = [chroms[c].regend // args.wstep for c in range(nch)]
+    seq_all = torch.repeat_interleave(torch.arange(nch, dtype=torch.int32, device=dev),
+                                      torch.tensor(wcount, device=dev))
+    start_all = torch.cat([torch.arange(w, dtype=torch.int64, device=dev) * args.wstep for w in wcount])
+    keep = scores != 0
+    sc, sd, seq, start = scores[keep], stddev[keep], seq_all[keep], start_all[keep]
+    ends = torch.tensor([chroms[c].regend - 1 for c in range(nch)], dtype=torch.int64, device=dev)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+
+    def run():
+        lim = fet_region_limit(sc, sd, 0.999, 75.0, stream=stream)
+        return lim, merge_regions(sc, seq, start, GD_SELECT_GE, lim[0], 100000, ends, stream=stream)
+
+    run()
+    torch.cuda.synchronize()
+    reps = 5
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        lim, (first, end, ns) = run()
+    ms = (time.perf_counter() - t0) * 1e3 / reps
+    res = {"what": "FilterFisherScores (limit + merge) on the device-resident FET track, 1 call",
+           "windows": int(sc.numel()), "ms": ms, "windows_per_s": sc.numel() / (ms * 1e-3),
+           "limit": lim[0], "selected": ns, "regions": int(len(first))}
+    if rank == 0 and world == 1 and not args.no_cpu:
+        sys.path.insert(0, str(ROOT / "oracle"))
+        import regions_oracle as ro
+        h_sc, h_sd = sc.cpu().numpy(), sd.cpu().numpy()
+        h_seq, h_start = seq.cpu().numpy(), start.cpu().numpy()
+        names = [str(k) for k in range(nch)]
+        c0 = time.perf_counter()
+        want = ro.filter_limit(h_sc, h_sd, 0.999, 75.0)
+        regs = ro.merge_regions([names[k] for k in h_seq], h_start, h_sc >= want[0], 100000,
+                                lambda s: chroms[int(s)].regend - 1)
+        cpu_ms = (time.perf_counter() - c0) * 1e3
+        res["cpu_baseline"] = {"value": sc.numel() / (cpu_ms * 1e-3), "unit": "windows/s", "cores": 1,
+                               "kind": "port", "sample": f"the whole track ({sc.numel()} windows), numpy + "
+                               "Python loop restatement (oracle/regions_oracle.py)"}
+        res["parity"] = bool(want[0] == lim[0] and [(int(f), int(e)) for f, e in zip(first, end)] == regs)
+    return res
+
+
 def main():
     args = parse()
     import torch
@@ -334,6 +382,8 @@ def main():
             out["roofline"]["traffic_source"] = f"{TRAFFIC_FILE.relative_to(ROOT)} ({tr['method']})"
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(args)
+
+    out["regions"] = regions_run(args, scores, stddev, chroms, nch, rank, world, dev)
 
     if not args.no_css:
         pv = torch.zeros_like(scores)
