@@ -55,8 +55,11 @@ __device__ unsigned long long g_css_prof[8];
 #endif
 
 /* waves per SIMD the register allocator must reach for k_css_mds<MP> (measured per
- * tier: the compile-time-K steps of MP <= 40 run best at 3-4 waves without spills) */
-#define CSS_MDS_WAVES(MP) ((MP) <= 24 ? 4 : (MP) <= 40 ? 3 : (MP) <= 64 ? 2 : (MP) <= 96 ? 3 : 2)
+ * tier: MP = 24 fits 5 waves without spills, MP = 40 runs best at 4 with a few cold
+ * spills) */
+#ifndef CSS_MDS_WAVES
+#define CSS_MDS_WAVES(MP) ((MP) <= 24 ? 5 : (MP) <= 40 ? 4 : (MP) <= 64 ? 2 : (MP) <= 96 ? 3 : 2)
+#endif
 
 namespace {
 
@@ -99,9 +102,14 @@ __device__ __forceinline__ double x86_int(double v) {
 /* wave64 reductions over DPP (quad_perm, row_ror, row_bcast): the total lands in
  * lane 63 and is read back as a wave-uniform scalar, so every lane holds the same
  * bits and control flow that depends on it stays uniform. */
+/* Lanes a row_mask leaves unwritten keep an undefined value (mov_dpp, no "old"
+ * operand, so no register has to be zeroed before every DPP move): every
+ * reduction below reads its result from lane 63, which only ever combines
+ * written lanes; full-mask steps write every lane. */
 template <int CTRL, int ROWMASK>
 __device__ __forceinline__ uint32_t dpp32(uint32_t v, uint32_t ident) {
-  return (uint32_t)__builtin_amdgcn_update_dpp((int)ident, (int)v, CTRL, ROWMASK, 0xF, false);
+  (void)ident;
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, ROWMASK, 0xF, false);
 }
 template <int CTRL, int ROWMASK>
 __device__ __forceinline__ double dpp64(double v, double ident) {
@@ -327,10 +335,14 @@ __device__ __forceinline__ void hh_step_static(double (&A)[MP], int m, int i, in
     s_d[K] = A[K];
   }
   __syncthreads();
-  if (K >= m - 2) {
+  if constexpr (K >= MP - 2) {
     if (tid == 0 && K == m - 2) s_e[K] = s_row[K + 1];
     return;
   }
+  /* K >= m - 2 (below MP - 2) runs the general step on the zero padding: x = 0, so
+   * sigma = 0, tau = 0, beta = alpha (= e_{m-2} at K = m - 2) and the update adds
+   * exact zeros -- the same values as an early exit, without a join point per step
+   * (each one cost a block of register moves) */
   const double xi = (i > K + 1 && row) ? s_row[ii] : 0.0;
   const double alpha = s_row[K + 1];
   double p0 = 0, p1 = 0;
@@ -387,7 +399,7 @@ struct HhStatic {
   static __device__ __forceinline__ void run(double (&A)[MP], int m, int i, int ii, int tid, bool row, double *s_row,
                                              double *s_v, double *s_w, double *s_d, double *s_e, double *s_tau,
                                              double *s_red) {
-    if (K >= m) return;
+    if ((K & 7) == 0 && K >= m) return; /* exits only at block boundaries (see above) */
     hh_step_static<MP, K>(A, m, i, ii, tid, row, s_row, s_v, s_w, s_d, s_e, s_tau, s_red);
     HhStatic<MP, K + 1>::run(A, m, i, ii, tid, row, s_row, s_v, s_w, s_d, s_e, s_tau, s_red);
   }

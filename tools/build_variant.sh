@@ -1,0 +1,15 @@
+#!/bin/bash
+# Build an A/B variant of libgdscan.so: csrc/gd_css_kernels.hip (or $SRC) recompiled with
+# extra flags, linked with the other objects of the regular build.
+# usage: tools/build_variant.sh NAME "-DGD_CSS_PROFILE ..."   -> tools/variants/NAME/libgdscan.so
+set -e
+NAME=$1; FLAGS=$2; SRC=${SRC:-gd_css_kernels}
+P=$(cd "$(dirname "$0")/.." && pwd)/fast-parallel-tools-for-genome-wide-analysis-of-genomic-divergence_amd
+OUT=$(dirname "$0")/variants/$NAME
+mkdir -p "$OUT"
+make -s -C "$P" >/dev/null
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -w $FLAGS \
+    -c "$P/csrc/$SRC.hip" -o "$OUT/$SRC.o"
+OBJS=$(ls "$P"/build/*.o | grep -v "/$SRC.o$")
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o "$OUT/libgdscan.so" $OBJS "$OUT/$SRC.o" -lpthread
+echo "$OUT/libgdscan.so"
