@@ -57,6 +57,9 @@ __device__ unsigned long long g_css_prof[8];
 /* waves per SIMD the register allocator must reach for k_css_mds<MP> (measured per
  * tier: MP = 24 fits 5 waves without spills, MP = 40 runs best at 4 with a few cold
  * spills) */
+#ifndef CSS_STATIC_G2_MAX
+#define CSS_STATIC_G2_MAX 80 /* largest G = 2 tier with compile-time-K steps */
+#endif
 #ifndef CSS_MDS_WAVES
 #define CSS_MDS_WAVES(MP) ((MP) <= 24 ? 5 : (MP) <= 40 ? 4 : (MP) <= 64 ? 2 : (MP) <= 96 ? 3 : 2)
 #endif
@@ -410,6 +413,117 @@ struct HhStatic<MP, MP> {
                                              double *, double *, double *, double *) {}
 };
 
+/* The compile-time-K step for the two-lanes-per-row tiers (G = 2): lane part h holds
+ * columns [h*CP, (h+1)*CP).  Block skipping is uniform over both parts (a block is
+ * skipped when it is dead in part 1), column K+1 and the dead column K sit at fixed
+ * registers of a fixed part, so reading A e_{K+1} and stashing v_K cost one select
+ * each instead of one per column. */
+template <int MP, int G, int K, int PART>
+__device__ __forceinline__ void hh_publish_part(const double (&A)[MP / G], double *s_row, double *s_d) {
+  constexpr int CP = MP / G, C0 = PART * CP;
+#pragma unroll
+  for (int jb = 0; jb < CP / 8; ++jb)
+    if ((G - 1) * CP + 8 * jb + 7 > K - 1) {
+#pragma unroll
+      for (int u = 0; u < 8; u += 2) {
+        const int j = C0 + 8 * jb + u;
+        *reinterpret_cast<double2 *>(s_row + j) =
+            make_double2(j > K ? A[8 * jb + u] : 0.0, j + 1 > K ? A[8 * jb + u + 1] : 0.0);
+      }
+    }
+  if constexpr (K >= C0 && K < C0 + CP) s_d[K] = A[K - C0];
+}
+
+template <int MP, int G, int K>
+__device__ __forceinline__ void hh_step_static_g(double (&A)[MP / G], int m, int i, int h, int ii, int tid,
+                                                 bool row, bool lead, double *s_row, double *s_v, double *s_w,
+                                                 double *s_d, double *s_e, double *s_tau, double *s_red) {
+  constexpr int CP = MP / G, NW = CssShape<MP, G>::NW;
+  const int c0 = h * CP;
+  __syncthreads();
+  if (i == K) {
+    if (h == 0)
+      hh_publish_part<MP, G, K, 0>(A, s_row, s_d);
+    else
+      hh_publish_part<MP, G, K, 1>(A, s_row, s_d);
+  }
+  __syncthreads();
+  if constexpr (K >= MP - 2) {
+    if (tid == 0 && K == m - 2) s_e[K] = s_row[K + 1];
+    return;
+  } else {
+    /* K >= m - 2 below MP - 2: a no-op reflector on the zero padding (hh_step_static) */
+    const double xi = (i > K + 1 && row) ? s_row[ii] : 0.0;
+    const double alpha = s_row[K + 1];
+    double p0 = 0, p1 = 0;
+#pragma unroll
+    for (int jb = 0; jb < CP / 8; ++jb) {
+      if ((G - 1) * CP + 8 * jb + 7 > K) {
+#pragma unroll
+        for (int u = 0; u < 8; u += 2) {
+          p0 = fma(A[8 * jb + u], s_row[c0 + 8 * jb + u], p0);
+          p1 = fma(A[8 * jb + u + 1], s_row[c0 + 8 * jb + u + 1], p1);
+        }
+        CSS_PIN(p0);
+        CSS_PIN(p1);
+      }
+    }
+    constexpr int HK1 = (K + 1) / CP, LK1 = K + 1 - HK1 * CP;
+    const double ak1 = pair_sum<G>(h == HK1 ? A[LK1] : 0.0);
+    const double sigma = block_sum<NW>(lead ? xi * xi : 0.0, s_red);
+    const double praw = pair_sum<G>(p0 + p1);
+    double tau = 0.0, beta = alpha, scale = 0.0;
+    if (sigma != 0.0) {
+      beta = -copysign(sqrt(alpha * alpha + sigma), alpha);
+      tau = (beta - alpha) * fast_rcp(beta);
+      scale = fast_rcp(alpha - beta);
+    }
+    const double vi = (i == K + 1) ? 1.0 : xi * scale;
+    const double pi = (i > K && row) ? (tau * scale) * fma(-beta, ak1, praw) : 0.0;
+    const double Kc = -0.5 * tau * block_sum<NW>(lead ? pi * vi : 0.0, s_red);
+    const double wi = fma(Kc, vi, pi);
+    if (tid == 0) {
+      s_e[K] = beta;
+      s_tau[K] = tau;
+    }
+    if (lead && i < MP) {
+      s_v[i] = vi;
+      s_w[i] = wi;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int jb = 0; jb < CP / 8; ++jb) {
+      if ((G - 1) * CP + 8 * jb + 7 > K) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int j = c0 + 8 * jb + u;
+          A[8 * jb + u] = fma(-vi, s_w[j], fma(-wi, s_v[j], A[8 * jb + u]));
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) CSS_PIN(A[8 * jb + u]);
+      }
+    }
+    constexpr int HK = K / CP, LK = K - HK * CP;
+    if (h == HK) A[LK] = vi; /* stash v_K in the dead column K */
+  }
+}
+
+template <int MP, int G, int K>
+struct HhStaticG {
+  static __device__ __forceinline__ void run(double (&A)[MP / G], int m, int i, int h, int ii, int tid, bool row,
+                                             bool lead, double *s_row, double *s_v, double *s_w, double *s_d,
+                                             double *s_e, double *s_tau, double *s_red) {
+    if ((K & 7) == 0 && K >= m) return;
+    hh_step_static_g<MP, G, K>(A, m, i, h, ii, tid, row, lead, s_row, s_v, s_w, s_d, s_e, s_tau, s_red);
+    HhStaticG<MP, G, K + 1>::run(A, m, i, h, ii, tid, row, lead, s_row, s_v, s_w, s_d, s_e, s_tau, s_red);
+  }
+};
+template <int MP, int G>
+struct HhStaticG<MP, G, MP> {
+  static __device__ __forceinline__ void run(double (&)[MP / G], int, int, int, int, int, bool, bool, double *,
+                                             double *, double *, double *, double *, double *, double *) {}
+};
+
 template <int MP, int G>
 __global__ void __launch_bounds__((CssShape<MP, G>::NT), CSS_MDS_WAVES(MP))
     k_css_mds(const gd_chrom_dev *ch, int nchrom, const gd_css_planes *pl, const uint32_t *planes,
@@ -615,6 +729,8 @@ __global__ void __launch_bounds__((CssShape<MP, G>::NT), CSS_MDS_WAVES(MP))
      * left of k) is skipped by a uniform branch. */
     if constexpr (G == 1 && MP <= 40) {
       HhStatic<MP, 0>::run(A, m, i, ii, tid, row, s_row, s_v, s_w, s_d, s_e, s_tau, s_red);
+    } else if constexpr (G == 2 && MP <= CSS_STATIC_G2_MAX) {
+      HhStaticG<MP, G, 0>::run(A, m, i, h, ii, tid, row, lead, s_row, s_v, s_w, s_d, s_e, s_tau, s_red);
     } else
     for (int k = 0; k < m; ++k) {
       __syncthreads();
