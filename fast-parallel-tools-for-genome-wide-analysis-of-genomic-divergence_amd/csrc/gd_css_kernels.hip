@@ -10,8 +10,7 @@
  *                matrix rows held in VGPRs, bisection for the two largest
  *                eigenvalues, inverse iteration, back-transformation, X = Q sqrt(L)
  *                (css.c:533-560), calc_dist + css (css.c:573-647).
- *   k_css_perm   significance_treshold (css.c:727-752): the early-exit permutation
- *                test on the window's distance matrix, staged in LDS.
+ *   (the permutation test, significance_treshold, is in gd_css_perm.hip)
  *
  * compare_all counts SNPs with (int)v_i * v_j == -9.  For the genotype codes
  * {3, 0, -3, -10000} that is exactly "one is 3 and the other -3", i.e.
@@ -1031,159 +1030,9 @@ __global__ void __launch_bounds__((CssShape<MP, G>::NT), CSS_MDS_WAVES(MP))
   }
 }
 
-/* ------------------------------------------------------------------------ */
-/* significance_treshold (css.c:727-752): early-exit Monte-Carlo p.            */
-/*                                                                            */
-/* Permutations run in batches of CSS_PB.  The batch's P*(m-1) nrand48 draws  */
-/* are generated in parallel (lane l starts at the l+1-th state via an affine */
-/* jump; a rejected draw, probability ~m/2^31, sends the batch through the    */
-/* serial generator instead).  Lane t < P applies the Fisher-Yates swaps of   */
-/* permutation t to an identity array (its position map sigma_t); the tracks  */
-/* after permutation t are F_t = F_{t-1} o sigma_t; the P separation scores   */
-/* are summed by groups of NT/P lanes; hits are counted in permutation order  */
-/* so the early exit stops exactly where the serial loop would.               */
-/* ------------------------------------------------------------------------ */
-#define CSS_PB 16
-
-template <int MP>
-__global__ void __launch_bounds__(64 * ((MP + 63) / 64))
-    k_css_perm(const gd_chrom_dev *ch, int nchrom, const double *xbuf, const uint8_t *status, int64_t wtotal,
-               int treshold, int runs, double *pvals) {
-  constexpr int NW = (MP + 63) / 64, NT = 64 * NW, P = CSS_PB, L = NT / P;
-  __shared__ double s_S[MP * MP];
-  __shared__ double s_x[2 * MP];
-  __shared__ uint8_t s_T[MP];      /* tracks before the batch */
-  __shared__ uint8_t s_r[P][MP];   /* draw s of permutation t (i = m-1-s, n = m-s) */
-  __shared__ uint8_t s_sig[P][MP]; /* position map of permutation t */
-  __shared__ uint8_t s_F[P][MP];   /* tracks after permutation t */
-  __shared__ gd_randint s_rd[MP + 1];
-  __shared__ double s_sc[P];
-  __shared__ uint64_t s_base;
-  const int i = threadIdx.x;
-  for (int n = i; n <= MP; n += NT) s_rd[n] = gd_randint_make(n < 1 ? 1u : (uint32_t)n);
-  const gd_affine J1 = gd_lcg_jump((uint64_t)i + 1), JN = gd_lcg_jump(NT);
-
-  for (int64_t w = blockIdx.x; w < wtotal; w += gridDim.x) {
-    if (!status[w]) continue;
-    const int c = chrom_of(ch, nchrom, w);
-    const gd_chrom_dev &d = ch[c];
-    const int a = d.asize, b = d.bsize, m = a + b, m1 = m - 1;
-    const int64_t wl = w - d.w_base;
-    __syncthreads();
-    if (i < 2 * MP) s_x[i] = xbuf[w * 2 * MP + i];
-    if (i + NT < 2 * MP) s_x[i + NT] = xbuf[w * 2 * MP + i + NT];
-    if (i < m) {
-      s_T[i] = (uint8_t)i;
-      s_F[0][i] = (uint8_t)i;
-    }
-    __syncthreads();
-    for (int e = i; e < m * m; e += NT) {
-      const int r = e / m, q = e - r * m;
-      s_S[e] = xdist(s_x, r, q);
-    }
-    __syncthreads();
-
-    /* css() of the first `np` composed track arrays -> s_sc[t] */
-    const double inva = a > 1 ? 1.0 / (double)(a * a * (a - 1)) : 0.0;
-    const double invb = b > 1 ? 1.0 / (double)(b * b * (b - 1)) : 0.0;
-    auto score_batch = [&](int np) {
-      const int t = i / L, l = i - t * L;
-      double bet = 0.0, win = 0.0;
-      if (t < np) {
-        const uint8_t *F = s_F[t];
-        for (int ii = l; ii < a; ii += L) {
-          const double *row = s_S + F[ii] * m;
-          for (int jj = 0; jj < b; ++jj) bet += row[F[a + jj]];
-        }
-        for (int ii = l; ii < a - 1; ii += L) win = fma(s_S[F[ii] * m + F[ii + 1]], inva, win);
-        for (int jj = l; jj < b - 1; jj += L) win = fma(s_S[F[a + jj] * m + F[a + jj + 1]], invb, win);
-      }
-#pragma unroll
-      for (int o = L / 2; o >= 1; o >>= 1) {
-        bet += __shfl_xor(bet, o);
-        win += __shfl_xor(win, o);
-      }
-      if (t < np && l == 0) s_sc[t] = bet / (a * b) - (a + b) * win;
-      __syncthreads();
-    };
-
-    score_batch(1); /* the observed score, summed exactly as the permuted ones */
-    const double obs = s_sc[0];
-    uint64_t base = gd_window_state(d.seed, GD_STREAM_CSS, wl);
-    const int nd = P * m1;
-    const gd_affine JB = gd_lcg_jump((uint64_t)nd);
-    int hits = 0, nsc = 0;
-    bool done = !(treshold > 0 && runs > 0);
-    while (!done) {
-      /* the batch's draws, assuming no rejection */
-      int rej = 0;
-      {
-        uint64_t x = gd_affine_apply(J1, base);
-        int t = i / m1, sidx = i - t * m1;
-        for (int q = i; q < nd; q += NT) {
-          const uint32_t r = gd_lcg_value(x);
-          const gd_randint rd = s_rd[m - sidx];
-          rej |= r > rd.limit;
-          s_r[t][sidx] = (uint8_t)gd_randint_mod(&rd, r);
-          x = gd_affine_apply(JN, x);
-          sidx += NT;
-          while (sidx >= m1) {
-            sidx -= m1;
-            ++t;
-          }
-        }
-      }
-      if (__syncthreads_or(rej)) {
-        if (i == 0) { /* exact serial generator for this batch */
-          uint64_t y = base;
-          for (int t = 0; t < P; ++t)
-            for (int sidx = 0; sidx < m1; ++sidx) {
-              const gd_randint rd = s_rd[m - sidx];
-              uint32_t r;
-              do {
-                y = gd_lcg_next(y);
-                r = gd_lcg_value(y);
-              } while (r > rd.limit);
-              s_r[t][sidx] = (uint8_t)gd_randint_mod(&rd, r);
-            }
-          s_base = y;
-        }
-        __syncthreads();
-        base = s_base;
-      } else {
-        base = gd_affine_apply(JB, base);
-      }
-      /* Fisher-Yates swaps of permutation t on an identity array */
-      if (i < P) {
-        uint8_t *arr = s_sig[i];
-        for (int p = 0; p < m; ++p) arr[p] = (uint8_t)p;
-        for (int sidx = 0; sidx < m1; ++sidx) {
-          const int ii = m1 - sidx, jj = s_r[i][sidx];
-          const uint8_t u = arr[ii], v = arr[jj];
-          arr[ii] = v;
-          arr[jj] = u;
-        }
-      }
-      __syncthreads();
-      /* F_t = F_{t-1} o sigma_t */
-      for (int t = 0; t < P; ++t) {
-        if (i < m) s_F[t][i] = (t == 0 ? s_T : s_F[t - 1])[s_sig[t][i]];
-        __syncthreads();
-      }
-      score_batch(P);
-      for (int t = 0; t < P && !done; ++t) {
-        hits += s_sc[t] >= obs;
-        ++nsc;
-        done = hits >= treshold || nsc >= runs;
-      }
-      if (!done) {
-        if (i < m) s_T[i] = s_F[P - 1][i];
-        __syncthreads();
-      }
-    }
-    if (i == 0) pvals[d.w_out + wl] = (hits + 1) * 1.0 / (nsc + 1);
-  }
-}
+/* the permutation test (gd_css_perm.hip) */
+int gd_css_perm_launch(int mp, const gd_chrom_dev *d_ch, int nchrom, const double *xbuf, const uint8_t *status,
+                       int64_t wtotal, int treshold, int runs, double *p, unsigned *wq, hipStream_t s);
 
 /* ------------------------------------------------------------------------ */
 int gd_css_tier(int m) {
@@ -1207,10 +1056,8 @@ static int launch_tier(const gd_chrom_dev *d_ch, int nchrom, const gd_css_planes
                      bvals, wtotal, want_x, force_literal, scores, p, xbuf, status, flags);
   if (hipGetLastError() != hipSuccess) return GD_ERR_HIP;
   if (want_x) {
-    hipLaunchKernelGGL(k_css_perm<MP>, dim3((unsigned)std::min<int64_t>(wtotal, 256 * 32)),
-                       dim3(64 * ((MP + 63) / 64)), 0, s, d_ch, nchrom, xbuf, status, wtotal,
-                       treshold, runs, p);
-    if (hipGetLastError() != hipSuccess) return GD_ERR_HIP;
+    const int st = gd_css_perm_launch(MP, d_ch, nchrom, xbuf, status, wtotal, treshold, runs, p, flags + 8, s);
+    if (st) return st;
   }
   return GD_OK;
 }
