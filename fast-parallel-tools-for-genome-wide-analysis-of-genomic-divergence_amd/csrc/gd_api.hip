@@ -49,10 +49,11 @@ int gd_fet_window_fast_launch(const gd_chrom_dev *ch, int nchrom, const int32_t 
                               const double *snp_score, double perc, double *scores, double *stddev,
                               unsigned *flags, int32_t *slow_list, unsigned *slow_count, hipStream_t s);
 int gd_css_tier(int m);
-int gd_css_launch(int mp, const gd_chrom_dev *d_ch, int nchrom, const gd_css_planes *d_pl, uint32_t *planes,
-                  const int32_t *lo_a, const int32_t *hi_a, const int32_t *lo_b, const double *avals,
-                  const double *bvals, int64_t wtotal, int64_t max_rows_words, int treshold, int runs,
-                  double *scores, double *p, double *xbuf, uint8_t *status, unsigned *flags, hipStream_t s);
+int gd_css_launch(int mp, int drosophila, int mds, const gd_chrom_dev *d_ch, int nchrom, const gd_css_planes *d_pl,
+                  uint32_t *planes, const int32_t *lo_a, const int32_t *hi_a, const int32_t *lo_b,
+                  const double *avals, const double *bvals, int64_t wtotal, int64_t max_rows_words, int treshold,
+                  int runs, double *scores, double *p, double *xbuf, uint8_t *status, unsigned *flags,
+                  hipStream_t s);
 int gd_synth_launch(int chrom, int nsnp, int asize, int bsize, uint64_t seed, const double *freq_table,
                     double *avals, double *bvals, int32_t *apos, int32_t *bpos, hipStream_t s);
 
@@ -464,7 +465,8 @@ static int host_scan(const double *avals, const double *bvals, const int *apos, 
 
 static int css_scan_locked(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, const double *avals,
                            const double *bvals, const int32_t *apos, const int32_t *bpos, int wsize, int wstep,
-                           int treshold, int runs, int window_set, double *scores, double *p, hipStream_t s);
+                           int treshold, int runs, int drosophila, int mds, int window_set, double *scores, double *p,
+                           hipStream_t s);
 
 /* several chromosomes from host memory in one device scan: H2D of the inputs and of
  * the caller's outputs (kept at uncomputed windows), the batched scan, D2H */
@@ -534,15 +536,23 @@ extern "C" int gd_fet_scan_host_batch(const gd_chrom *chroms, int nchrom, const 
                     });
 }
 
-extern "C" int gd_css_scan_host_batch(const gd_chrom *chroms, int nchrom, const double *avals, const double *bvals,
-                                      const int *apos, const int *bpos, int wsize, int wstep, int treshold,
-                                      int runs, int window_set, double *scores, double *p) {
+extern "C" int gd_css_scan_host_batch_ex(const gd_chrom *chroms, int nchrom, const double *avals,
+                                         const double *bvals, const int *apos, const int *bpos, int wsize, int wstep,
+                                         int treshold, int runs, int drosophila, int mds, int window_set,
+                                         double *scores, double *p) {
   return host_batch(chroms, nchrom, avals, bvals, apos, bpos, wstep, scores, p,
                     [&](gd_ctx *ctx, double *av, double *bv, int32_t *ap, int32_t *bp, double *o0, double *o1,
                         hipStream_t s) {
                       return css_scan_locked(ctx, chroms, nchrom, av, bv, ap, bp, wsize, wstep, treshold, runs,
-                                             window_set, o0, o1, s);
+                                             drosophila, mds, window_set, o0, o1, s);
                     });
+}
+
+extern "C" int gd_css_scan_host_batch(const gd_chrom *chroms, int nchrom, const double *avals, const double *bvals,
+                                      const int *apos, const int *bpos, int wsize, int wstep, int treshold,
+                                      int runs, int window_set, double *scores, double *p) {
+  return gd_css_scan_host_batch_ex(chroms, nchrom, avals, bvals, apos, bpos, wsize, wstep, treshold, runs, 0, 0,
+                                   window_set, scores, p);
 }
 
 extern "C" int gd_fet_scan_host(const double *avals, const double *bvals, const int *apos, const int *bpos,
@@ -576,7 +586,10 @@ extern "C" int gd_fet_compute(const double *avals, const double *bvals, const in
 /* --------------------------------------------------------------- CSS scan */
 static int css_scan_locked(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, const double *avals,
                            const double *bvals, const int32_t *apos, const int32_t *bpos, int wsize, int wstep,
-                           int treshold, int runs, int window_set, double *scores, double *p, hipStream_t s) {
+                           int treshold, int runs, int drosophila, int mds, int window_set, double *scores, double *p,
+                           hipStream_t s) {
+  if (drosophila != 0 && drosophila != 1) return fail(GD_ERR_ARG, "drosophila must be 0 or 1");
+  if (mds < 0 || mds > 2) return fail(GD_ERR_ARG, "mds must be 0 (classical), 1 (SMACOF) or 2 (SMACOF + classical)");
   ScanPlan pl;
   int st = make_plan(chroms, nchrom, wsize, wstep, window_set, &pl);
   if (st) return st;
@@ -641,8 +654,15 @@ static int css_scan_locked(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, cons
     max_words = std::max(max_words, std::max(wa * d.asize, wb * d.bsize));
   }
   const int mp = gd_css_tier(mmax);
-  if (mp == 0) return fail(GD_ERR_SIZE, "asize + bsize above the largest supported CSS tier (96)");
-  const bool perms = runs > 0 && treshold > 0;
+  if (mp == 0) return fail(GD_ERR_SIZE, "asize + bsize above the largest supported CSS tier (128)");
+  if (drosophila)
+    for (int c = 0; c < nchrom; ++c) {
+      const gd_chrom_dev &d = pl.h[c];
+      if (d.wend > 0 && d.asize > 0 && d.bsize > 0 && (d.asize != 1 || d.bsize != 1))
+        return fail(GD_ERR_ARG, "the drosophila metric compares one allele frequency per population "
+                                "(asize = bsize = 1; compare_freq, css.c:245-264)");
+    }
+  const bool perms = (runs > 0 && treshold > 0) || mds == 2; /* xbuf/status carry coordinates */
   auto layout2 = [&](Carve &k, gd_css_planes **d_pl, uint32_t **planes, double **xbuf, uint8_t **status) {
     layout1(k, &d_ch, &flags, &lo_a, &hi_a, &lo_b);
     *d_pl = k.take<gd_css_planes>(nchrom);
@@ -678,8 +698,8 @@ static int css_scan_locked(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, cons
   HIP_TRY(hipMemsetAsync(planes, 0, sizeof(uint32_t) * std::max<int64_t>(words, 1), s));
   if (perms) HIP_TRY(hipMemsetAsync(status, 0, pl.wtotal, s));
   HIP_TRY(hipEventRecord(ctx->ev[1], s));
-  st = gd_css_launch(mp, d_ch, nchrom, d_pl, planes, lo_a, hi_a, lo_b, avals, bvals, pl.wtotal, max_words,
-                     treshold, runs, scores, p, xbuf, status, flags, s);
+  st = gd_css_launch(mp, drosophila, mds, d_ch, nchrom, d_pl, planes, lo_a, hi_a, lo_b, avals, bvals, pl.wtotal,
+                     max_words, treshold, runs, scores, p, xbuf, status, flags, s);
   if (st) return fail(st, "CSS kernel launch failed");
   HIP_TRY(hipEventRecord(ctx->ev[3], s));
   HIP_TRY(hipMemcpyAsync(ctx->h_flags, flags, 16 * sizeof(unsigned), hipMemcpyDeviceToHost, s));
@@ -693,46 +713,58 @@ static int css_scan_locked(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, cons
 
 /* CSS needs the window bounds and sizes laid out by css_scan_locked; the
  * pipeline reads them back from the context's workspace */
+extern "C" int gd_css_scan_device_ex(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, const double *avals,
+                                     const double *bvals, const int32_t *apos, const int32_t *bpos, int wsize,
+                                     int wstep, int treshold, int runs, int drosophila, int mds, int window_set,
+                                     double *scores, double *p, void *hip_stream) {
+  if (!ctx) return fail(GD_ERR_ARG, "null context");
+  std::lock_guard<std::mutex> g(ctx->mu);
+  return css_scan_locked(ctx, chroms, nchrom, avals, bvals, apos, bpos, wsize, wstep, treshold, runs, drosophila, mds,
+                         window_set, scores, p, (hipStream_t)hip_stream);
+}
+
 extern "C" int gd_css_scan_device(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, const double *avals,
                                   const double *bvals, const int32_t *apos, const int32_t *bpos, int wsize,
                                   int wstep, int treshold, int runs, int window_set, double *scores, double *p,
                                   void *hip_stream) {
-  if (!ctx) return fail(GD_ERR_ARG, "null context");
-  std::lock_guard<std::mutex> g(ctx->mu);
-  return css_scan_locked(ctx, chroms, nchrom, avals, bvals, apos, bpos, wsize, wstep, treshold, runs, window_set,
-                         scores, p, (hipStream_t)hip_stream);
+  return gd_css_scan_device_ex(ctx, chroms, nchrom, avals, bvals, apos, bpos, wsize, wstep, treshold, runs, 0, 0,
+                               window_set, scores, p, hip_stream);
+}
+
+extern "C" int gd_css_scan_host_ex(const double *avals, const double *bvals, const int *apos, const int *bpos,
+                                   int regend, int wsize, int wstep, int alen, int blen, int treshold, int runs,
+                                   int drosophila, int mds, uint64_t seed, int window_set, double *scores,
+                                   double *p) {
+  return host_scan(avals, bvals, apos, bpos, regend, wsize, wstep, alen, blen, scores, p,
+                   [&](gd_ctx *ctx, gd_chrom *ch, double *av, double *bv, int32_t *ap, int32_t *bp, double *o0,
+                       double *o1, hipStream_t s) {
+                     ch->seed = seed;
+                     return css_scan_locked(ctx, ch, 1, av, bv, ap, bp, wsize, wstep, treshold, runs, drosophila,
+                                            mds, window_set, o0, o1, s);
+                   });
 }
 
 extern "C" int gd_css_scan_host(const double *avals, const double *bvals, const int *apos, const int *bpos,
                                 int regend, int wsize, int wstep, int alen, int blen, int treshold, int runs,
                                 uint64_t seed, int window_set, double *scores, double *p) {
-  return host_scan(avals, bvals, apos, bpos, regend, wsize, wstep, alen, blen, scores, p,
-                   [&](gd_ctx *ctx, gd_chrom *ch, double *av, double *bv, int32_t *ap, int32_t *bp, double *o0,
-                       double *o1, hipStream_t s) {
-                     ch->seed = seed;
-                     return css_scan_locked(ctx, ch, 1, av, bv, ap, bp, wsize, wstep, treshold, runs, window_set,
-                                            o0, o1, s);
-                   });
+  return gd_css_scan_host_ex(avals, bvals, apos, bpos, regend, wsize, wstep, alen, blen, treshold, runs, 0, 0, seed,
+                             window_set, scores, p);
 }
 
 extern "C" int gd_css_threadcompute(const double *avals, const double *bvals, const int *apos, const int *bpos,
                                     int regstart, int regend, int wsize, int wstep, int alen, int blen,
                                     int treshold, int runs, int drosophila, int mds, double *scores, double *p) {
-  (void)regstart;
-  if (drosophila != 0 || mds != 0)
-    return fail(GD_ERR_ARG, "only the count metric (drosophila=0) with classical MDS (mds=0) is implemented");
-  return gd_css_scan_host(avals, bvals, apos, bpos, regend, wsize, wstep, alen, blen, treshold, runs,
-                          g_seed.load(), GD_WINDOWS_THREADED, scores, p);
+  (void)regstart; /* ignored by the reference too (threadcss.c) */
+  return gd_css_scan_host_ex(avals, bvals, apos, bpos, regend, wsize, wstep, alen, blen, treshold, runs, drosophila,
+                             mds, g_seed.load(), GD_WINDOWS_THREADED, scores, p);
 }
 
 extern "C" int gd_css_compute(const double *avals, const double *bvals, const int *apos, const int *bpos,
                               int regstart, int regend, int wsize, int wstep, int alen, int blen, int treshold,
                               int runs, int drosophila, int mds, double *scores, double *p) {
-  (void)regstart;
-  if (drosophila != 0 || mds != 0)
-    return fail(GD_ERR_ARG, "only the count metric (drosophila=0) with classical MDS (mds=0) is implemented");
-  return gd_css_scan_host(avals, bvals, apos, bpos, regend, wsize, wstep, alen, blen, treshold, runs,
-                          g_seed.load(), GD_WINDOWS_SERIAL, scores, p);
+  (void)regstart; /* ignored by the reference too (css.c:78) */
+  return gd_css_scan_host_ex(avals, bvals, apos, bpos, regend, wsize, wstep, alen, blen, treshold, runs, drosophila,
+                             mds, g_seed.load(), GD_WINDOWS_SERIAL, scores, p);
 }
 
 /* ------------------------------------------------------------- utilities */

@@ -77,11 +77,13 @@ GD_HD uint64_t gd_affine_apply(gd_affine f, uint64_t x) { return (f.mul * x + f.
 /* threadfisher.c:186-188, threadcss.c:221-223, so its stddev/p are not        */
 /* reproducible).  Every window gets its own 48-bit nrand48 state:             */
 /*   x0(seed, stream, w) = mix64(seed ^ mix64(stream + PHI*(w+1))) mod 2^48     */
-/* stream 0 = FET bootstrap, stream 1 = CSS permutations.  The state words an  */
-/* nrand48 caller would hold are {x0 & 0xffff, (x0>>16) & 0xffff, x0 >> 32}.   */
+/* stream 0 = FET bootstrap, stream 1 = CSS permutations, stream 2 = SMACOF   */
+/* starts.  The state words an nrand48 caller would hold are                  */
+/* {x0 & 0xffff, (x0>>16) & 0xffff, x0 >> 32}.                                */
 /* ------------------------------------------------------------------------- */
 #define GD_STREAM_FET 0ULL
 #define GD_STREAM_CSS 1ULL
+#define GD_STREAM_SMACOF 2ULL /* drand48 starts of smacof_runs (css.c:818-821) */
 
 GD_HD uint64_t gd_mix64(uint64_t z) {
   z ^= z >> 30;
@@ -236,12 +238,14 @@ GD_HD void gd_table_opposite_extreme(int *f) {
   ((double)((uint64_t)BINOM((a) + (b), (a)) * (uint64_t)BINOM((c) + (d), (c))) / \
    (double)BINOM((a) + (b) + (c) + (d), (a) + (c)))
 
-#define GD_DEFINE_FET(NAME, QUAL, BINOM)                                     \
+#define GD_DEFINE_FET(NAME, QUAL, BINOM) GD_DEFINE_FET_P(NAME, QUAL, BINOM, GD_FET_TABLE_P)
+/* TABLEP(BINOM, a, b, c, d): probability of one table (GD_FET_TABLE_P or an exact form) */
+#define GD_DEFINE_FET_P(NAME, QUAL, BINOM, TABLEP)                                     \
   QUAL double NAME(int a, int b, int c, int d) {                             \
     const int tie = (a + b == c + d) || (a + c == b + d);                    \
     int f[4] = {a, b, c, d};                                                 \
     gd_table_min_to_a(f);                                                    \
-    const double p0 = GD_FET_TABLE_P(BINOM, f[0], f[1], f[2], f[3]);         \
+    const double p0 = TABLEP(BINOM, f[0], f[1], f[2], f[3]);                  \
     double tot = p0, step = p0;                                              \
     while (f[0] > 0) {                                                       \
       f[1]++;                                                                \
@@ -256,7 +260,7 @@ GD_HD void gd_table_opposite_extreme(int *f) {
     } else {                                                                 \
       gd_table_opposite_extreme(f);                                          \
       gd_table_min_to_a(f);                                                  \
-      double far = GD_FET_TABLE_P(BINOM, f[0], f[1], f[2], f[3]);            \
+      double far = TABLEP(BINOM, f[0], f[1], f[2], f[3]);                     \
       while (far < p0) {                                                     \
         tot += far;                                                          \
         if (f[1] == 0 || f[2] == 0) break;                                   \
@@ -365,6 +369,50 @@ GD_DEV double gd_log10_glibc(double x) {
   x = gd_f64_from(((uint64_t)(uint32_t)hx << 32) | lx);
   const double z = y * log10_2lo + ivln10 * gd_log_reduced(x);
   return z + y * log10_2hi;
+}
+
+/* ------------------------------------------------------------------------- */
+/* FET table-probability modes.  The kernels receive one table buffer:        */
+/*   [0, GD_BINOM_ENTRIES)        binomial(n, k) as the reference computes it   */
+/*   [GD_FET_MODE_WORD]           0 = reference, 1 = exact                      */
+/*   [GD_FET_LF_OFF, +2*256)      ln k!, k <= 255, as double-double (hi, lo)    */
+/* Reference mode: fet_p = C(a+b,a) C(c+d,c) / C(n,a+c) in u64 (cFisher.c:     */
+/* 473-483), wrapping / 0 where the reference's unsigned long overflows (first */
+/* at C(68,31)).  Exact mode: the same tail algorithm  */
+/* over P = exp(sum of +-ln k!) with the sum in double-double: finite and      */
+/* accurate to ~1e-13 relative for every table the u64 path overflows on.      */
+/* ------------------------------------------------------------------------- */
+#define GD_FET_MODE_WORD GD_BINOM_ENTRIES
+#define GD_FET_LF_OFF (GD_BINOM_ENTRIES + 1)
+#define GD_FET_TAB_WORDS (GD_BINOM_ENTRIES + 1 + 2 * (GD_BINOM_NMAX + 1))
+
+GD_HD gd_dd gd_dd_neg(gd_dd a) {
+  gd_dd r;
+  r.hi = -a.hi;
+  r.lo = -a.lo;
+  return r;
+}
+
+/* C(a+b, a) C(c+d, c) / C(n, a+c) from the ln k! table (lf_hi / lf_lo, k <= 255) */
+GD_DEV double gd_fet_table_p_exact(const double *lf_hi, const double *lf_lo, int a, int b, int c, int d) {
+  const int n = a + b + c + d;
+  gd_dd s = {0.0, 0.0};
+  if (n <= GD_BINOM_NMAX) {
+    const int pos[4] = {a + b, c + d, a + c, b + d};
+    const int neg[5] = {a, b, c, d, n};
+    for (int k = 0; k < 4; ++k) {
+      const gd_dd t = {lf_hi[pos[k]], lf_lo[pos[k]]};
+      s = gd_dd_add(s, t);
+    }
+    for (int k = 0; k < 5; ++k) {
+      const gd_dd t = {lf_hi[neg[k]], lf_lo[neg[k]]};
+      s = gd_dd_add(s, gd_dd_neg(t));
+    }
+  } else {
+    s.hi = lgamma(a + b + 1.0) + lgamma(c + d + 1.0) + lgamma(a + c + 1.0) + lgamma(b + d + 1.0) -
+           lgamma(a + 1.0) - lgamma(b + 1.0) - lgamma(c + 1.0) - lgamma(d + 1.0) - lgamma(n + 1.0);
+  }
+  return exp(s.hi) * (1.0 + s.lo);
 }
 
 /* per-SNP score: -1.0 * log10(p)  (cFisher.c:183) */

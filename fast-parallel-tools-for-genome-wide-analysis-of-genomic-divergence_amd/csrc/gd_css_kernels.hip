@@ -1030,9 +1030,18 @@ __global__ void __launch_bounds__((CssShape<MP, G>::NT), CSS_MDS_WAVES(MP))
   }
 }
 
-/* the permutation test (gd_css_perm.hip) */
+/* the other stages of a scan (gd_css_perm.hip, gd_css_smacof.hip) */
 int gd_css_perm_launch(int mp, const gd_chrom_dev *d_ch, int nchrom, const double *xbuf, const uint8_t *status,
                        int64_t wtotal, int treshold, int runs, double *p, unsigned *wq, hipStream_t s);
+int gd_css_smacof_launch(int mp, bool freq, const gd_chrom_dev *d_ch, int nchrom, const gd_css_planes *d_pl,
+                         const uint32_t *planes, const int32_t *lo_a, const int32_t *hi_a, const int32_t *lo_b,
+                         const double *avals, const double *bvals, int64_t wtotal, int mds, int want_x,
+                         int force_literal, double *scores, double *p, double *xbuf, uint8_t *status,
+                         unsigned *flags, hipStream_t s);
+int gd_css_freq_cmds_launch(int mp, const gd_chrom_dev *d_ch, int nchrom, const int32_t *lo_a, const int32_t *hi_a,
+                            const int32_t *lo_b, const double *avals, const double *bvals, int64_t wtotal,
+                            int want_x, double *scores, double *p, double *xbuf, uint8_t *status, unsigned *flags,
+                            hipStream_t s);
 
 /* ------------------------------------------------------------------------ */
 int gd_css_tier(int m) {
@@ -1045,29 +1054,30 @@ int gd_css_tier(int m) {
 template <int MP, int G>
 static int launch_tier(const gd_chrom_dev *d_ch, int nchrom, const gd_css_planes *d_pl, const uint32_t *planes,
                        const int32_t *lo_a, const int32_t *hi_a, const int32_t *lo_b, const double *avals,
-                       const double *bvals, int64_t wtotal, int treshold, int runs, double *scores, double *p,
+                       const double *bvals, int64_t wtotal, int want_x, int force_literal, double *scores, double *p,
                        double *xbuf, uint8_t *status, unsigned *flags, hipStream_t s) {
   constexpr int NT = CssShape<MP, G>::NT;
-  const int want_x = (runs > 0 && treshold > 0) ? 1 : 0;
-  const unsigned gx = (unsigned)wtotal;
-  const char *fl = getenv("GD_CSS_FORCE_LITERAL"); /* diagnostics: per-SNP predicate for every window */
-  const int force_literal = (fl && fl[0] == '1') ? 1 : 0;
-  hipLaunchKernelGGL((k_css_mds<MP, G>), dim3(gx), dim3(NT), 0, s, d_ch, nchrom, d_pl, planes, lo_a, hi_a, lo_b, avals,
-                     bvals, wtotal, want_x, force_literal, scores, p, xbuf, status, flags);
-  if (hipGetLastError() != hipSuccess) return GD_ERR_HIP;
-  if (want_x) {
-    const int st = gd_css_perm_launch(MP, d_ch, nchrom, xbuf, status, wtotal, treshold, runs, p, flags + 8, s);
-    if (st) return st;
-  }
-  return GD_OK;
+  hipLaunchKernelGGL((k_css_mds<MP, G>), dim3((unsigned)wtotal), dim3(NT), 0, s, d_ch, nchrom, d_pl, planes, lo_a,
+                     hi_a, lo_b, avals, bvals, wtotal, want_x, force_literal, scores, p, xbuf, status, flags);
+  return hipGetLastError() == hipSuccess ? GD_OK : GD_ERR_HIP;
 }
 
-int gd_css_launch(int mp, const gd_chrom_dev *d_ch, int nchrom, const gd_css_planes *d_pl, uint32_t *planes,
-                  const int32_t *lo_a, const int32_t *hi_a, const int32_t *lo_b, const double *avals,
-                  const double *bvals, int64_t wtotal, int64_t max_rows_words, int treshold, int runs,
-                  double *scores, double *p, double *xbuf, uint8_t *status, unsigned *flags,
+/* One CSS scan after the window bounds: bit planes, the scores of the chosen metric
+ * and MDS (cluster_separation_scorer, css.c:181-223), the permutation test.
+ *   mds 0: k_css_mds (count metric) or k_css_freq_cmds (drosophila)
+ *   mds 1: k_css_smacof from drand48 starts
+ *   mds 2: the classical stage, then k_css_smacof from its coordinates (xbuf)
+ * xbuf/status carry the coordinates between stages when runs > 0 or mds == 2. */
+int gd_css_launch(int mp, int drosophila, int mds, const gd_chrom_dev *d_ch, int nchrom, const gd_css_planes *d_pl,
+                  uint32_t *planes, const int32_t *lo_a, const int32_t *hi_a, const int32_t *lo_b,
+                  const double *avals, const double *bvals, int64_t wtotal, int64_t max_rows_words, int treshold,
+                  int runs, double *scores, double *p, double *xbuf, uint8_t *status, unsigned *flags,
                   hipStream_t s) {
-  {
+  const bool perms = runs > 0 && treshold > 0;
+  const int want_x1 = (perms || mds == 2) ? 1 : 0; /* coordinates out of the classical stage */
+  const char *fl = getenv("GD_CSS_FORCE_LITERAL"); /* diagnostics: per-SNP predicate for every window */
+  const int force_literal = (fl && fl[0] == '1') ? 1 : 0;
+  if (!drosophila) {
     const unsigned gx = (unsigned)std::min<int64_t>((max_rows_words * 8 + 255) / 256, std::max(1, 16384 / nchrom));
     hipLaunchKernelGGL(k_css_pack, dim3(std::max(1u, gx), nchrom, 2), dim3(256), 0, s, d_ch, d_pl, avals, bvals,
                        planes);
@@ -1089,25 +1099,36 @@ int gd_css_launch(int mp, const gd_chrom_dev *d_ch, int nchrom, const gd_css_pla
     }
   } dump{s};
 #endif
-  switch (mp) {
-    case 24:
-      return launch_tier<24, 1>(d_ch, nchrom, d_pl, planes, lo_a, hi_a, lo_b, avals, bvals, wtotal, treshold, runs,
-                             scores, p, xbuf, status, flags, s);
-    case 40:
-      return launch_tier<40, 1>(d_ch, nchrom, d_pl, planes, lo_a, hi_a, lo_b, avals, bvals, wtotal, treshold, runs,
-                             scores, p, xbuf, status, flags, s);
-    case 64:
-      return launch_tier<64, 1>(d_ch, nchrom, d_pl, planes, lo_a, hi_a, lo_b, avals, bvals, wtotal, treshold, runs,
-                             scores, p, xbuf, status, flags, s);
-    case 80:
-      return launch_tier<80, 2>(d_ch, nchrom, d_pl, planes, lo_a, hi_a, lo_b, avals, bvals, wtotal, treshold, runs,
-                             scores, p, xbuf, status, flags, s);
-    case 96:
-      return launch_tier<96, 2>(d_ch, nchrom, d_pl, planes, lo_a, hi_a, lo_b, avals, bvals, wtotal, treshold, runs,
-                             scores, p, xbuf, status, flags, s);
-    case 128:
-      return launch_tier<128, 2>(d_ch, nchrom, d_pl, planes, lo_a, hi_a, lo_b, avals, bvals, wtotal, treshold,
-                                 runs, scores, p, xbuf, status, flags, s);
+  int st = GD_OK;
+  if (mds != 1) {
+    if (drosophila) {
+      st = gd_css_freq_cmds_launch(mp, d_ch, nchrom, lo_a, hi_a, lo_b, avals, bvals, wtotal, want_x1, scores, p, xbuf,
+                                   status, flags, s);
+    } else {
+#define CSS_TIER(T, G)                                                                                          \
+  case T:                                                                                                       \
+    st = launch_tier<T, G>(d_ch, nchrom, d_pl, planes, lo_a, hi_a, lo_b, avals, bvals, wtotal, want_x1,         \
+                           force_literal, scores, p, xbuf, status, flags, s);                                   \
+    break;
+      switch (mp) {
+        CSS_TIER(24, 1)
+        CSS_TIER(40, 1)
+        CSS_TIER(64, 1)
+        CSS_TIER(80, 2)
+        CSS_TIER(96, 2)
+        CSS_TIER(128, 2)
+        default:
+          return GD_ERR_SIZE;
+      }
+#undef CSS_TIER
+    }
+    if (st) return st;
   }
-  return GD_ERR_SIZE;
+  if (mds != 0) {
+    st = gd_css_smacof_launch(mp, drosophila != 0, d_ch, nchrom, d_pl, planes, lo_a, hi_a, lo_b, avals, bvals, wtotal,
+                              mds, perms ? 1 : 0, force_literal, scores, p, xbuf, status, flags, s);
+    if (st) return st;
+  }
+  if (perms) st = gd_css_perm_launch(mp, d_ch, nchrom, xbuf, status, wtotal, treshold, runs, p, flags + 8, s);
+  return st;
 }

@@ -29,9 +29,10 @@ GD_SELECT_LE = 1
 # every symbol include/gdscan.h declares
 EXPORTS = (
     "gd_fet_threadcompute", "gd_fet_compute", "gd_fet_scan_host",
-    "gd_css_threadcompute", "gd_css_compute", "gd_css_scan_host",
+    "gd_css_threadcompute", "gd_css_compute", "gd_css_scan_host", "gd_css_scan_host_ex",
     "gd_ctx_create", "gd_ctx_destroy", "gd_window_count",
-    "gd_fet_scan_device", "gd_css_scan_device", "gd_fet_scan_host_batch", "gd_css_scan_host_batch",
+    "gd_fet_scan_device", "gd_css_scan_device", "gd_css_scan_device_ex", "gd_fet_scan_host_batch",
+    "gd_css_scan_host_batch", "gd_css_scan_host_batch_ex",
     "gd_set_seed", "gd_get_seed", "gd_last_error", "gd_device_count",
     "gd_last_stage_ms", "gd_synth_device",
     "gd_gtrack_read", "gd_gtrack_free", "gd_gtrack_nseq", "gd_gtrack_seqid", "gd_gtrack_len", "gd_gtrack_copy",
@@ -73,6 +74,8 @@ def _load() -> C.CDLL:
     lib.gd_css_threadcompute.argtypes = css_ref
     lib.gd_css_compute.argtypes = css_ref
     lib.gd_css_scan_host.argtypes = [dp, dp, ip, ip, i32, i32, i32, i32, i32, i32, i32, C.c_uint64, i32, dp, dp]
+    lib.gd_css_scan_host_ex.argtypes = [dp, dp, ip, ip, i32, i32, i32, i32, i32, i32, i32, i32, i32, C.c_uint64, i32,
+                                        dp, dp]
     lib.gd_ctx_create.argtypes = [i32]
     lib.gd_ctx_create.restype = vp
     lib.gd_ctx_destroy.argtypes = [vp]
@@ -82,6 +85,8 @@ def _load() -> C.CDLL:
                                        vp, vp, vp]
     lib.gd_css_scan_device.argtypes = [vp, C.POINTER(Chrom), i32, vp, vp, vp, vp, i32, i32, i32, i32, i32,
                                        vp, vp, vp]
+    lib.gd_css_scan_device_ex.argtypes = [vp, C.POINTER(Chrom), i32, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32,
+                                          i32, vp, vp, vp]
     lib.gd_set_seed.argtypes = [C.c_uint64]
     lib.gd_set_seed.restype = None
     lib.gd_get_seed.restype = C.c_uint64
@@ -90,6 +95,9 @@ def _load() -> C.CDLL:
     lib.gd_synth_device.argtypes = [i32, i32, i32, i32, C.c_uint64, vp, vp, vp, vp, vp, vp]
     lib.gd_fet_scan_host_batch.argtypes = [C.POINTER(Chrom), i32, dp, dp, ip, ip, i32, i32, C.c_double, i32, dp, dp]
     lib.gd_css_scan_host_batch.argtypes = [C.POINTER(Chrom), i32, dp, dp, ip, ip, i32, i32, i32, i32, i32, dp, dp]
+    lib.gd_css_scan_host_batch_ex.argtypes = [C.POINTER(Chrom), i32, dp, dp, ip, ip, i32, i32, i32, i32, i32, i32, i32,
+                                              dp, dp]
+    lib.gd_css_scan_host_batch_ex.restype = C.c_int
     lib.gd_fet_scan_host_batch.restype = C.c_int
     lib.gd_css_scan_host_batch.restype = C.c_int
     lib.gd_gtrack_read.argtypes = [C.c_char_p]
@@ -125,7 +133,8 @@ def _load() -> C.CDLL:
     for fn in ("gd_gtrack_nseq", "gd_gtrack_copy", "gd_write_tabular", "gd_format_py2_float"):
         getattr(lib, fn).restype = C.c_int
     for fn in ("gd_fet_threadcompute", "gd_fet_compute", "gd_fet_scan_host", "gd_css_threadcompute",
-               "gd_css_compute", "gd_css_scan_host", "gd_fet_scan_device", "gd_css_scan_device",
+               "gd_css_compute", "gd_css_scan_host", "gd_css_scan_host_ex", "gd_fet_scan_device",
+               "gd_css_scan_device", "gd_css_scan_device_ex",
                "gd_synth_device", "gd_device_count", "gd_window_count", "gd_last_stage_ms"):
         getattr(lib, fn).restype = C.c_int
     return lib

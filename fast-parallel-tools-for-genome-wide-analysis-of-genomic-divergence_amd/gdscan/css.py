@@ -43,15 +43,17 @@ def cluster_separation_scorer_serial(avals, bvals, apos, bpos, regstart, regend,
          drosophila, mds, scores, p)
 
 
-def scan(avals, bvals, apos, bpos, regend, wsize=2500, wstep=500, treshold=10, runs=0, seed=None, serial=False):
+def scan(avals, bvals, apos, bpos, regend, wsize=2500, wstep=500, treshold=10, runs=0, seed=None, serial=False,
+         drosophila=0, mds=0):
+    """One chromosome; drosophila / mds as cluster_separation_scorer (css.c:181-223)."""
     nwin = int(regend) // int(wstep)
     scores = np.zeros(nwin)
     p = np.zeros(nwin)
     (av, bv, ap, bp), scores, p = _ptrs(avals, bvals, apos, bpos, scores, p, "p")
     s = lib.gd_get_seed() if seed is None else int(seed)
-    check(lib.gd_css_scan_host(av.ctypes.data_as(_DP), bv.ctypes.data_as(_DP), ap.ctypes.data_as(_IP),
-                               bp.ctypes.data_as(_IP), int(regend), int(wsize), int(wstep), av.shape[0],
-                               bv.shape[0], int(treshold), int(runs), s,
-                               GD_WINDOWS_SERIAL if serial else GD_WINDOWS_THREADED,
-                               scores.ctypes.data_as(_DP), p.ctypes.data_as(_DP)))
+    check(lib.gd_css_scan_host_ex(av.ctypes.data_as(_DP), bv.ctypes.data_as(_DP), ap.ctypes.data_as(_IP),
+                                  bp.ctypes.data_as(_IP), int(regend), int(wsize), int(wstep), av.shape[0],
+                                  bv.shape[0], int(treshold), int(runs), int(drosophila), int(mds), s,
+                                  GD_WINDOWS_SERIAL if serial else GD_WINDOWS_THREADED,
+                                  scores.ctypes.data_as(_DP), p.ctypes.data_as(_DP)))
     return scores, p

@@ -63,17 +63,26 @@ def fisher_exact_test_snp(track_a, track_b, out_path, wsize=2500, wstep=500, per
     return names, scores, stddev
 
 
+# ClusterSeparationScore.py:167-173: the distance metric and MDS choices of the tool
+COMPARE = {"count": 0, "Count individual SNP-differences in window": 0, "freq": 1}
+MDS = {"classical": 0, "Classical MDS": 0, "smacof": 1, "SMACOF": 1, "smacof+cmds": 2}
+
+
 def cluster_separation_score(track_a, track_b, out_path, wsize=2500, wstep=500, mc_treshold=10, mc_runs=0,
                              compare="count", mds="classical", chrom_lengths=None):
+    """compare: "count" (SNP differences) or "freq" (drosophila allele-frequency metric,
+    one frequency track per population); mds: "classical", "smacof" or "smacof+cmds"
+    (any other label selects SMACOF + classical, as the tool's else branch does)."""
     import ctypes as C
-    if compare != "count" or mds != "classical":
-        raise ValueError("only the count metric with classical MDS is implemented (DESIGN.md section 6)")
+    if compare not in COMPARE:
+        raise ValueError(f"unknown distance metric {compare!r}")
+    dro, md = COMPARE[compare], MDS.get(mds, 2)
     names, chroms, av, bv, ap, bp, w = _batch(track_a, track_b, wstep, chrom_lengths)
     scores, p = np.zeros(w), np.zeros(w)
     if names:
-        check(lib.gd_css_scan_host_batch(chroms, len(names), _ptr(av, C.c_double), _ptr(bv, C.c_double),
-                                         _ptr(ap, C.c_int), _ptr(bp, C.c_int), int(wsize), int(wstep),
-                                         int(mc_treshold), int(mc_runs), GD_WINDOWS_THREADED,
-                                         _ptr(scores, C.c_double), _ptr(p, C.c_double)))
+        check(lib.gd_css_scan_host_batch_ex(chroms, len(names), _ptr(av, C.c_double), _ptr(bv, C.c_double),
+                                            _ptr(ap, C.c_int), _ptr(bp, C.c_int), int(wsize), int(wstep),
+                                            int(mc_treshold), int(mc_runs), dro, md, GD_WINDOWS_THREADED,
+                                            _ptr(scores, C.c_double), _ptr(p, C.c_double)))
     _write(out_path, "#seqid\tstart\tscore\tp", names, chroms, wstep, scores, p)
     return names, scores, p

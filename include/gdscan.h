@@ -70,6 +70,16 @@ int gd_css_compute(const double *avals, const double *bvals, const int *apos, co
 int gd_css_scan_host(const double *avals, const double *bvals, const int *apos, const int *bpos, int regend,
                      int wsize, int wstep, int alen, int blen, int treshold, int runs, uint64_t seed,
                      int window_set, double *scores, double *p);
+/* with the reference's options (cluster_separation_scorer, css.c:181-223):
+ *   drosophila 1: compare_freq (css.c:245-264), mean |a - b| of the two populations'
+ *                 allele frequencies; needs asize = bsize = 1 (else GD_ERR_ARG: the
+ *                 reference fills only D[0][1] and reads uninitialised memory)
+ *   mds 0: classical MDS; 1: SMACOF from 4 drand48 starts (smacof_runs, css.c:807-835);
+ *   2: classical MDS refined by one SMACOF run (css.c:211-213).  The SMACOF starts of
+ *   window w come from drand48 stream (seed, w, 2) (the reference: time-seeded). */
+int gd_css_scan_host_ex(const double *avals, const double *bvals, const int *apos, const int *bpos, int regend,
+                        int wsize, int wstep, int alen, int blen, int treshold, int runs, int drosophila, int mds,
+                        uint64_t seed, int window_set, double *scores, double *p);
 
 /* ---- device-resident batched scans (all pointers are device pointers except `chroms`) ---- */
 typedef struct gd_chrom {
@@ -95,6 +105,10 @@ int gd_fet_scan_device(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, const do
 int gd_css_scan_device(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, const double *avals, const double *bvals,
                        const int32_t *apos, const int32_t *bpos, int wsize, int wstep, int treshold, int runs,
                        int window_set, double *scores, double *p, void *hip_stream);
+int gd_css_scan_device_ex(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, const double *avals,
+                          const double *bvals, const int32_t *apos, const int32_t *bpos, int wsize, int wstep,
+                          int treshold, int runs, int drosophila, int mds, int window_set, double *scores, double *p,
+                          void *hip_stream);
 
 /* the same batch from host memory (offsets into host arrays; outputs are caller-owned
  * host arrays holding every chromosome's w_out + regend/wstep windows) */
@@ -104,6 +118,9 @@ int gd_fet_scan_host_batch(const gd_chrom *chroms, int nchrom, const double *ava
 int gd_css_scan_host_batch(const gd_chrom *chroms, int nchrom, const double *avals, const double *bvals,
                            const int *apos, const int *bpos, int wsize, int wstep, int treshold, int runs,
                            int window_set, double *scores, double *p);
+int gd_css_scan_host_batch_ex(const gd_chrom *chroms, int nchrom, const double *avals, const double *bvals,
+                              const int *apos, const int *bpos, int wsize, int wstep, int treshold, int runs,
+                              int drosophila, int mds, int window_set, double *scores, double *p);
 
 /* ---- region filters after the scan ----
  * A track is the list of windows a tool's tabular file holds (score != 0), in file

@@ -39,4 +39,16 @@ int orc_css_scan(const double *avals, const double *bvals, const int *apos, cons
                  int wstep, int alen, int blen, int treshold, int runs, uint64_t seed, int serial, double *scores,
                  double *p);
 
+/* CSS options (css_options_oracle.c) */
+void orc_css_compare_freq(const double *av, const double *bv, int npos, double *D);
+double orc_css_stress(const double *delta, const double *D, int m);
+double orc_css_smacof(const double *delta, int m, double *X, int max_iters, double epsilon, int *iters);
+double orc_css_smacof_runs(const double *delta, int m, double *X, uint64_t state48);
+int orc_css_window_ex(const double *av, const double *bv, int asize, int bsize, int npos, int treshold, int runs,
+                      int drosophila, int mds, uint64_t perm48, uint64_t smacof48, double *score, double *p,
+                      int *nperm);
+int orc_css_scan_ex(const double *avals, const double *bvals, const int *apos, const int *bpos, int regend,
+                    int wsize, int wstep, int alen, int blen, int treshold, int runs, int drosophila, int mds,
+                    uint64_t seed, int serial, double *scores, double *p);
+
 #endif

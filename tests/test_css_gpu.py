@@ -99,17 +99,6 @@ def test_reference_entry_point_in_place(oracle):
     assert np.all(p[s_ref == 0] == -7.0)  # untouched at uncomputed windows
 
 
-def test_unsupported_options_raise():
-    import css_cython_parallel as ccp
-    from gdscan import GdError
-    av, bv, ap, bp, regend = _synth(9, 6_000, 4, 4)
-    out = np.zeros(regend // 500)
-    for dro, mds in ((1, 0), (0, 1), (0, 2)):
-        with pytest.raises(GdError):
-            ccp.cluster_separation_scorer(av, bv, ap, bp, 0, regend, 2500, 500, len(av), len(bv), 10, 0, dro, mds,
-                                          out, out.copy())
-
-
 def test_cohort_above_largest_tier_raises():
     from gdscan import GdError, css
     av, bv, ap, bp, regend = _synth(10, 2_000, 70, 70)
