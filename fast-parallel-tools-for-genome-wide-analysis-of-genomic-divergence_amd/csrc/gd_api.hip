@@ -14,6 +14,7 @@
 #include <algorithm>
 #include <atomic>
 #include <cstdio>
+#include <cmath>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -32,7 +33,7 @@ __global__ void k_snp_fet(const gd_chrom_dev *ch, const double *avals, const dou
                           const int *lut_hdr, const double *lut, double *snp_score);
 __global__ void k_fet_lut_build(const gd_chrom_dev *ch, const uint64_t *binom, const int *hdr, double *lut,
                                 int64_t cap);
-__global__ void k_fet_lut_publish(const gd_chrom_dev *ch, int *hdr, int64_t cap);
+__global__ void k_fet_lut_publish(const gd_chrom_dev *ch, const uint64_t *binom, int *hdr, int64_t cap);
 template <int BLOCK, bool GLOBAL_SCRATCH>
 __global__ void k_fet_window_general(const gd_chrom_dev *ch, int nchrom, const int32_t *wlist,
                                      const unsigned *wlist_count, int64_t wtotal, const int32_t *lo_a,
@@ -60,6 +61,7 @@ int gd_synth_launch(int chrom, int nsnp, int asize, int bsize, uint64_t seed, co
 /* ------------------------------------------------------------------ errors */
 static thread_local std::string g_err;
 static std::atomic<uint64_t> g_seed{GD_DEFAULT_SEED};
+static std::atomic<int> g_fet_mode{GD_FET_REFERENCE};
 static thread_local float g_stage_ms[GD_NSTAGES];
 
 static int fail(int code, const std::string &msg) {
@@ -86,7 +88,8 @@ struct gd_ctx {
   size_t ws_cap = 0;
   double *gscratch = nullptr;
   size_t gscratch_cap = 0; /* doubles */
-  uint64_t *binom = nullptr;
+  uint64_t *binom = nullptr;       /* FET table buffer (gd_common.h), reference mode */
+  uint64_t *binom_exact = nullptr; /* the same, exact mode */
   /* FET score table, cached across scans for the last (asize, bsize) */
   int *lut_hdr = nullptr;
   double *lut = nullptr;
@@ -109,9 +112,28 @@ static int ctx_init(gd_ctx *c, int device) {
     HIP_TRY(hipStreamCreateWithPriority(&c->stream_mem, hipStreamNonBlocking, greatest));
   }
   for (auto &e : c->gev) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-  HIP_TRY(hipMalloc(&c->binom, sizeof(uint64_t) * GD_BINOM_ENTRIES));
+  HIP_TRY(hipMalloc(&c->binom, sizeof(uint64_t) * GD_FET_TAB_WORDS));
+  HIP_TRY(hipMalloc(&c->binom_exact, sizeof(uint64_t) * GD_FET_TAB_WORDS));
   hipLaunchKernelGGL(k_binom_table, dim3((GD_BINOM_ENTRIES + 255) / 256), dim3(256), 0, c->stream, c->binom);
+  hipLaunchKernelGGL(k_binom_table, dim3((GD_BINOM_ENTRIES + 255) / 256), dim3(256), 0, c->stream, c->binom_exact);
   HIP_TRY(hipGetLastError());
+  {
+    /* behind the binomials (disjoint from the kernel's writes): the mode word, then
+     * ln k! as double-double for exact mode */
+    std::vector<uint64_t> tail(GD_FET_TAB_WORDS - GD_BINOM_ENTRIES, 0);
+    tail[0] = GD_FET_REFERENCE;
+    HIP_TRY(hipMemcpy(c->binom + GD_BINOM_ENTRIES, tail.data(), sizeof(uint64_t) * tail.size(),
+                      hipMemcpyHostToDevice));
+    tail[0] = GD_FET_EXACT;
+    for (int k = 0; k <= GD_BINOM_NMAX; ++k) {
+      const long double L = lgammal((long double)k + 1.0L);
+      const double hi = (double)L, lo = (double)(L - (long double)hi);
+      std::memcpy(&tail[GD_FET_LF_OFF - GD_BINOM_ENTRIES + k], &hi, sizeof hi);
+      std::memcpy(&tail[GD_FET_LF_OFF - GD_BINOM_ENTRIES + GD_BINOM_NMAX + 1 + k], &lo, sizeof lo);
+    }
+    HIP_TRY(hipMemcpy(c->binom_exact + GD_BINOM_ENTRIES, tail.data(), sizeof(uint64_t) * tail.size(),
+                      hipMemcpyHostToDevice));
+  }
   for (auto &e : c->ev) HIP_TRY(hipEventCreate(&e));
   HIP_TRY(hipMalloc(&c->lut_hdr, 4 * sizeof(int)));
   HIP_TRY(hipMemsetAsync(c->lut_hdr, 0, 4 * sizeof(int), c->stream));
@@ -137,6 +159,7 @@ extern "C" void gd_ctx_destroy(gd_ctx *c) {
   (void)hipFree(c->ws);
   (void)hipFree(c->gscratch);
   (void)hipFree(c->binom);
+  (void)hipFree(c->binom_exact);
   (void)hipFree(c->lut_hdr);
   (void)hipFree(c->lut);
   (void)hipFree(c->io);
@@ -268,8 +291,11 @@ static int flags_to_status(unsigned f) {
 /* --------------------------------------------------------------- FET scan */
 static int fet_scan_locked(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, const double *avals,
                            const double *bvals, const int32_t *apos, const int32_t *bpos, int wsize, int wstep,
-                           double perc, int window_set, double *scores, double *stddev, hipStream_t s) {
+                           double perc, int mode, int window_set, double *scores, double *stddev, hipStream_t s) {
   if (!(perc >= 0.0 && perc <= 1.0)) return fail(GD_ERR_ARG, "percentile must lie in [0, 1]");
+  if (mode != GD_FET_REFERENCE && mode != GD_FET_EXACT)
+    return fail(GD_ERR_ARG, "FET mode must be GD_FET_REFERENCE (0) or GD_FET_EXACT (1)");
+  const uint64_t *binom = mode == GD_FET_EXACT ? ctx->binom_exact : ctx->binom;
   ScanPlan pl;
   int st = make_plan(chroms, nchrom, wsize, wstep, window_set, &pl);
   if (st) return st;
@@ -320,9 +346,9 @@ static int fet_scan_locked(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, cons
   bool force_general = false;
   if ((st = gd_fet_window_prepare(pl.wtotal, list, list_count, sm, &force_general))) return st;
   /* score table for chromosome 0's population sizes (no-op when cached) */
-  hipLaunchKernelGGL(k_fet_lut_build, dim3(512), dim3(256), 0, sm, d_ch, ctx->binom, ctx->lut_hdr, ctx->lut,
+  hipLaunchKernelGGL(k_fet_lut_build, dim3(512), dim3(256), 0, sm, d_ch, binom, ctx->lut_hdr, ctx->lut,
                      (int64_t)GD_LUT_CAP);
-  hipLaunchKernelGGL(k_fet_lut_publish, dim3(1), dim3(1), 0, sm, d_ch, ctx->lut_hdr, (int64_t)GD_LUT_CAP);
+  hipLaunchKernelGGL(k_fet_lut_publish, dim3(1), dim3(1), 0, sm, d_ch, binom, ctx->lut_hdr, (int64_t)GD_LUT_CAP);
 
   int G = std::min(nchrom, GD_MAX_GROUPS);
   if (const char *eg = getenv("GD_GROUPS")) G = std::max(1, std::min(G, atoi(eg))); /* diagnostics */
@@ -340,7 +366,7 @@ static int fet_scan_locked(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, cons
     hipLaunchKernelGGL(k_bounds, dim3(gxb, nc, 2), dim3(256), 0, sm, d_ch + c0, apos, bpos, wsize, wstep, lo_a,
                        hi_a, lo_b, flags);
     const unsigned gxs = (unsigned)std::min<int64_t>((amax + 255) / 256, std::max(1, 8192 / nc));
-    hipLaunchKernelGGL(k_snp_fet, dim3(gxs, nc), dim3(256), 0, sm, d_ch + c0, avals, bvals, ctx->binom,
+    hipLaunchKernelGGL(k_snp_fet, dim3(gxs, nc), dim3(256), 0, sm, d_ch + c0, avals, bvals, binom,
                        ctx->lut_hdr, ctx->lut, snp);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(ctx->gev[g], sm));
@@ -360,7 +386,7 @@ static int fet_scan_locked(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, cons
     /* windows the fast path declined: literal one-workgroup-per-window path */
     const unsigned gx = (unsigned)std::min<int64_t>(pl.wtotal, 4096);
     hipLaunchKernelGGL((k_fet_window_general<64, false>), dim3(gx), dim3(64), 0, s, d_ch, nchrom, list,
-                       list_count, pl.wtotal, lo_a, hi_a, lo_b, avals, bvals, snp, ctx->binom, perc, scores,
+                       list_count, pl.wtotal, lo_a, hi_a, lo_b, avals, bvals, snp, binom, perc, scores,
                        stddev, flags, huge, huge_count, (double *)nullptr, (int64_t)0);
   }
   HIP_TRY(hipGetLastError());
@@ -383,7 +409,7 @@ static int fet_scan_locked(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, cons
       ctx->gscratch_cap = per * slots;
     }
     hipLaunchKernelGGL((k_fet_window_general<256, true>), dim3(slots), dim3(256), 0, s, d_ch, nchrom, huge,
-                       huge_count, (int64_t)0, lo_a, hi_a, lo_b, avals, bvals, snp, ctx->binom, perc, scores,
+                       huge_count, (int64_t)0, lo_a, hi_a, lo_b, avals, bvals, snp, binom, perc, scores,
                        stddev, flags, (int32_t *)nullptr, (unsigned *)nullptr, ctx->gscratch, per);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipMemcpyAsync(ctx->h_flags, flags, 16 * sizeof(unsigned), hipMemcpyDeviceToHost, s));
@@ -399,14 +425,22 @@ static int fet_scan_locked(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, cons
   return flags_to_status(ctx->h_flags[0]);
 }
 
+extern "C" int gd_fet_scan_device_ex(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, const double *avals,
+                                     const double *bvals, const int32_t *apos, const int32_t *bpos, int wsize,
+                                     int wstep, double perc, int mode, int window_set, double *scores,
+                                     double *stddev, void *hip_stream) {
+  if (!ctx) return fail(GD_ERR_ARG, "null context");
+  std::lock_guard<std::mutex> g(ctx->mu);
+  return fet_scan_locked(ctx, chroms, nchrom, avals, bvals, apos, bpos, wsize, wstep, perc, mode, window_set,
+                         scores, stddev, (hipStream_t)hip_stream);
+}
+
 extern "C" int gd_fet_scan_device(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, const double *avals,
                                   const double *bvals, const int32_t *apos, const int32_t *bpos, int wsize,
                                   int wstep, double perc, int window_set, double *scores, double *stddev,
                                   void *hip_stream) {
-  if (!ctx) return fail(GD_ERR_ARG, "null context");
-  std::lock_guard<std::mutex> g(ctx->mu);
-  return fet_scan_locked(ctx, chroms, nchrom, avals, bvals, apos, bpos, wsize, wstep, perc, window_set, scores,
-                         stddev, (hipStream_t)hip_stream);
+  return gd_fet_scan_device_ex(ctx, chroms, nchrom, avals, bvals, apos, bpos, wsize, wstep, perc,
+                               g_fet_mode.load(), window_set, scores, stddev, hip_stream);
 }
 
 /* one chromosome from host memory: H2D, device scan, D2H of the outputs */
@@ -525,15 +559,22 @@ static int host_batch(const gd_chrom *chroms, int nchrom, const double *avals, c
   return GD_OK;
 }
 
-extern "C" int gd_fet_scan_host_batch(const gd_chrom *chroms, int nchrom, const double *avals, const double *bvals,
-                                      const int *apos, const int *bpos, int wsize, int wstep, double perc,
-                                      int window_set, double *scores, double *stddev) {
+extern "C" int gd_fet_scan_host_batch_ex(const gd_chrom *chroms, int nchrom, const double *avals,
+                                         const double *bvals, const int *apos, const int *bpos, int wsize, int wstep,
+                                         double perc, int mode, int window_set, double *scores, double *stddev) {
   return host_batch(chroms, nchrom, avals, bvals, apos, bpos, wstep, scores, stddev,
                     [&](gd_ctx *ctx, double *av, double *bv, int32_t *ap, int32_t *bp, double *o0, double *o1,
                         hipStream_t s) {
-                      return fet_scan_locked(ctx, chroms, nchrom, av, bv, ap, bp, wsize, wstep, perc, window_set,
-                                             o0, o1, s);
+                      return fet_scan_locked(ctx, chroms, nchrom, av, bv, ap, bp, wsize, wstep, perc, mode,
+                                             window_set, o0, o1, s);
                     });
+}
+
+extern "C" int gd_fet_scan_host_batch(const gd_chrom *chroms, int nchrom, const double *avals, const double *bvals,
+                                      const int *apos, const int *bpos, int wsize, int wstep, double perc,
+                                      int window_set, double *scores, double *stddev) {
+  return gd_fet_scan_host_batch_ex(chroms, nchrom, avals, bvals, apos, bpos, wsize, wstep, perc, g_fet_mode.load(),
+                                   window_set, scores, stddev);
 }
 
 extern "C" int gd_css_scan_host_batch_ex(const gd_chrom *chroms, int nchrom, const double *avals,
@@ -555,16 +596,25 @@ extern "C" int gd_css_scan_host_batch(const gd_chrom *chroms, int nchrom, const 
                                    window_set, scores, p);
 }
 
-extern "C" int gd_fet_scan_host(const double *avals, const double *bvals, const int *apos, const int *bpos,
-                                int regend, int wsize, int wstep, int alen, int blen, double perc, uint64_t seed,
-                                int window_set, double *scores, double *stddev) {
+extern "C" int gd_fet_scan_host_ex(const double *avals, const double *bvals, const int *apos, const int *bpos,
+                                   int regend, int wsize, int wstep, int alen, int blen, double perc, int mode,
+                                   uint64_t seed, int window_set, double *scores, double *stddev) {
+  if (mode != GD_FET_REFERENCE && mode != GD_FET_EXACT)
+    return fail(GD_ERR_ARG, "FET mode must be GD_FET_REFERENCE (0) or GD_FET_EXACT (1)");
   return host_scan(avals, bvals, apos, bpos, regend, wsize, wstep, alen, blen, scores, stddev,
                    [&](gd_ctx *ctx, gd_chrom *ch, double *av, double *bv, int32_t *ap, int32_t *bp, double *o0,
                        double *o1, hipStream_t s) {
                      ch->seed = seed;
-                     return fet_scan_locked(ctx, ch, 1, av, bv, ap, bp, wsize, wstep, perc, window_set, o0,
+                     return fet_scan_locked(ctx, ch, 1, av, bv, ap, bp, wsize, wstep, perc, mode, window_set, o0,
                                             o1, s);
                    });
+}
+
+extern "C" int gd_fet_scan_host(const double *avals, const double *bvals, const int *apos, const int *bpos,
+                                int regend, int wsize, int wstep, int alen, int blen, double perc, uint64_t seed,
+                                int window_set, double *scores, double *stddev) {
+  return gd_fet_scan_host_ex(avals, bvals, apos, bpos, regend, wsize, wstep, alen, blen, perc, g_fet_mode.load(),
+                             seed, window_set, scores, stddev);
 }
 
 extern "C" int gd_fet_threadcompute(const double *avals, const double *bvals, const int *apos, const int *bpos,
@@ -770,6 +820,12 @@ extern "C" int gd_css_compute(const double *avals, const double *bvals, const in
 /* ------------------------------------------------------------- utilities */
 extern "C" void gd_set_seed(uint64_t seed) { g_seed.store(seed); }
 extern "C" uint64_t gd_get_seed(void) { return g_seed.load(); }
+extern "C" int gd_set_fet_mode(int mode) {
+  if (mode != GD_FET_REFERENCE && mode != GD_FET_EXACT)
+    return fail(GD_ERR_ARG, "FET mode must be GD_FET_REFERENCE (0) or GD_FET_EXACT (1)");
+  return g_fet_mode.exchange(mode);
+}
+extern "C" int gd_get_fet_mode(void) { return g_fet_mode.load(); }
 extern "C" const char *gd_last_error(void) { return g_err.c_str(); }
 extern "C" int gd_device_count(void) {
   int n = 0;

@@ -238,9 +238,10 @@ GD_HD void gd_table_opposite_extreme(int *f) {
   ((double)((uint64_t)BINOM((a) + (b), (a)) * (uint64_t)BINOM((c) + (d), (c))) / \
    (double)BINOM((a) + (b) + (c) + (d), (a) + (c)))
 
-#define GD_DEFINE_FET(NAME, QUAL, BINOM) GD_DEFINE_FET_P(NAME, QUAL, BINOM, GD_FET_TABLE_P)
-/* TABLEP(BINOM, a, b, c, d): probability of one table (GD_FET_TABLE_P or an exact form) */
-#define GD_DEFINE_FET_P(NAME, QUAL, BINOM, TABLEP)                                     \
+#define GD_DEFINE_FET(NAME, QUAL, BINOM) GD_DEFINE_FET_P(NAME, QUAL, BINOM, GD_FET_TABLE_P, 0.0)
+/* TABLEP(BINOM, a, b, c, d): probability of one table (GD_FET_TABLE_P or an exact form);
+ * TIE: relative tie tolerance of the far tail (0 reproduces the reference) */
+#define GD_DEFINE_FET_P(NAME, QUAL, BINOM, TABLEP, TIE)                                     \
   QUAL double NAME(int a, int b, int c, int d) {                             \
     const int tie = (a + b == c + d) || (a + c == b + d);                    \
     int f[4] = {a, b, c, d};                                                 \
@@ -261,7 +262,7 @@ GD_HD void gd_table_opposite_extreme(int *f) {
       gd_table_opposite_extreme(f);                                          \
       gd_table_min_to_a(f);                                                  \
       double far = TABLEP(BINOM, f[0], f[1], f[2], f[3]);                     \
-      while (far < p0) {                                                     \
+      while (far < p0 * (1.0 - (TIE))) {                                                     \
         tot += far;                                                          \
         if (f[1] == 0 || f[2] == 0) break;                                   \
         f[0]++;                                                              \
@@ -385,6 +386,11 @@ GD_DEV double gd_log10_glibc(double x) {
 #define GD_FET_MODE_WORD GD_BINOM_ENTRIES
 #define GD_FET_LF_OFF (GD_BINOM_ENTRIES + 1)
 #define GD_FET_TAB_WORDS (GD_BINOM_ENTRIES + 1 + 2 * (GD_BINOM_NMAX + 1))
+/* Exact mode counts a far-tail table whose probability lies within this relative distance
+ * of the observed table's as a tie and stops there, as the reference's `far < p0` does on
+ * its exactly rounded u64 quotients; otherwise the rounding of the ln k! sums would decide
+ * ties (e.g. table (1, 6, 8, 6)). */
+#define GD_FET_EXACT_TIE 1e-9
 
 GD_HD gd_dd gd_dd_neg(gd_dd a) {
   gd_dd r;

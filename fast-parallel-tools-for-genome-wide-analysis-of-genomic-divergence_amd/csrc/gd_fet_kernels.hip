@@ -33,12 +33,20 @@ struct BinomTab {
   __device__ __forceinline__ uint64_t operator()(int n, int k) const { return binom_at(t, n, k); }
 };
 
+/* the table buffer's mode word (reference / exact, gd_common.h) */
+__device__ __forceinline__ int fet_mode(const uint64_t *tab) { return (int)tab[GD_FET_MODE_WORD]; }
+
 __device__ double fet_p_two_tailed(int a, int b, int c, int d, const uint64_t *tab) {
   BinomTab B{tab};
+  const bool exact = fet_mode(tab) != 0;
+  const double *lfh = reinterpret_cast<const double *>(tab + GD_FET_LF_OFF), *lfl = lfh + (GD_BINOM_NMAX + 1);
+  auto table_p = [&](const int *g) {
+    return exact ? gd_fet_table_p_exact(lfh, lfl, g[0], g[1], g[2], g[3]) : GD_FET_TABLE_P(B, g[0], g[1], g[2], g[3]);
+  };
   const int tie = (a + b == c + d) || (a + c == b + d);
   int f[4] = {a, b, c, d};
   gd_table_min_to_a(f);
-  const double p0 = GD_FET_TABLE_P(B, f[0], f[1], f[2], f[3]);
+  const double p0 = table_p(f);
   double tot = p0, step = p0;
   while (f[0] > 0) {
     f[1]++;
@@ -53,8 +61,8 @@ __device__ double fet_p_two_tailed(int a, int b, int c, int d, const uint64_t *t
   } else {
     gd_table_opposite_extreme(f);
     gd_table_min_to_a(f);
-    double far = GD_FET_TABLE_P(B, f[0], f[1], f[2], f[3]);
-    while (far < p0) {
+    double far = table_p(f);
+    while (far < (exact ? p0 * (1.0 - GD_FET_EXACT_TIE) : p0)) {
       tot += far;
       if (f[1] == 0 || f[2] == 0) break;
       f[0]++;
@@ -277,7 +285,8 @@ __global__ void __launch_bounds__(256) k_snp_fet(const gd_chrom_dev *ch, const d
   const gd_chrom_dev &d = ch[blockIdx.y];
   if (d.wend <= 0) return;
   const int nrows = d.nrows, asize = d.asize, bsize = d.bsize;
-  const bool use_lut = lut_hdr[2] == 1 && lut_hdr[0] == asize && lut_hdr[1] == bsize;
+  const bool use_lut =
+      lut_hdr[2] == 1 && lut_hdr[0] == asize && lut_hdr[1] == bsize && lut_hdr[3] == fet_mode(binom);
   const int lut_nb = (bsize + 1) * (bsize + 2) / 2;
   const int big = max(asize, bsize);
   const int R = min(256, ((SF_MAXCH - 2) * 128) / max(big, 1));
@@ -338,13 +347,13 @@ __global__ void __launch_bounds__(256) k_snp_fet(const gd_chrom_dev *ch, const d
 /* code as above (so a lookup is bit-identical to a direct evaluation).  Built */
 /* once per (asize, bsize) and kept in the context; k_snp_fet then only counts */
 /* and gathers.  20+20 individuals: 231 x 231 = 53,361 tables (427 KB, L2).    */
-/* hdr = {asize, bsize, valid}.                                                */
+/* hdr = {asize, bsize, valid, mode}.                                               */
 /* ------------------------------------------------------------------------ */
 __global__ void __launch_bounds__(256) k_fet_lut_build(const gd_chrom_dev *ch, const uint64_t *binom,
                                                        const int *hdr, double *lut, int64_t cap) {
   const int asize = ch[0].asize, bsize = ch[0].bsize;
   if (asize <= 0 || bsize <= 0) return;
-  if (hdr[2] == 1 && hdr[0] == asize && hdr[1] == bsize) return; /* cached */
+  if (hdr[2] == 1 && hdr[0] == asize && hdr[1] == bsize && hdr[3] == fet_mode(binom)) return; /* cached */
   const int64_t na = (int64_t)(asize + 1) * (asize + 2) / 2, nb = (int64_t)(bsize + 1) * (bsize + 2) / 2;
   if (na * nb > cap) return;
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < na * nb; e += (int64_t)gridDim.x * blockDim.x) {
@@ -362,13 +371,14 @@ __global__ void __launch_bounds__(256) k_fet_lut_build(const gd_chrom_dev *ch, c
   }
 }
 
-__global__ void k_fet_lut_publish(const gd_chrom_dev *ch, int *hdr, int64_t cap) {
+__global__ void k_fet_lut_publish(const gd_chrom_dev *ch, const uint64_t *binom, int *hdr, int64_t cap) {
   const int asize = ch[0].asize, bsize = ch[0].bsize;
   const int64_t na = (int64_t)(asize + 1) * (asize + 2) / 2, nb = (int64_t)(bsize + 1) * (bsize + 2) / 2;
   const bool ok = asize > 0 && bsize > 0 && na * nb <= cap;
   hdr[0] = asize;
   hdr[1] = bsize;
   hdr[2] = ok ? 1 : 0;
+  hdr[3] = fet_mode(binom);
 }
 
 /* ------------------------------------------------------------------------ */

@@ -25,10 +25,13 @@ GD_WINDOWS_SERIAL = 1
 GD_NSTAGES = 4
 GD_SELECT_GE = 0
 GD_SELECT_LE = 1
+GD_FET_REFERENCE = 0
+GD_FET_EXACT = 1
 
 # every symbol include/gdscan.h declares
 EXPORTS = (
-    "gd_fet_threadcompute", "gd_fet_compute", "gd_fet_scan_host",
+    "gd_fet_threadcompute", "gd_fet_compute", "gd_fet_scan_host", "gd_fet_scan_host_ex",
+    "gd_set_fet_mode", "gd_get_fet_mode", "gd_fet_scan_device_ex", "gd_fet_scan_host_batch_ex",
     "gd_css_threadcompute", "gd_css_compute", "gd_css_scan_host", "gd_css_scan_host_ex",
     "gd_ctx_create", "gd_ctx_destroy", "gd_window_count",
     "gd_fet_scan_device", "gd_css_scan_device", "gd_css_scan_device_ex", "gd_fet_scan_host_batch",
@@ -71,6 +74,10 @@ def _load() -> C.CDLL:
     lib.gd_fet_threadcompute.argtypes = fet_ref
     lib.gd_fet_compute.argtypes = fet_ref
     lib.gd_fet_scan_host.argtypes = [dp, dp, ip, ip, i32, i32, i32, i32, i32, C.c_double, C.c_uint64, i32, dp, dp]
+    lib.gd_fet_scan_host_ex.argtypes = [dp, dp, ip, ip, i32, i32, i32, i32, i32, C.c_double, i32, C.c_uint64, i32,
+                                        dp, dp]
+    lib.gd_set_fet_mode.argtypes = [i32]
+    lib.gd_get_fet_mode.argtypes = []
     lib.gd_css_threadcompute.argtypes = css_ref
     lib.gd_css_compute.argtypes = css_ref
     lib.gd_css_scan_host.argtypes = [dp, dp, ip, ip, i32, i32, i32, i32, i32, i32, i32, C.c_uint64, i32, dp, dp]
@@ -83,6 +90,8 @@ def _load() -> C.CDLL:
     lib.gd_window_count.argtypes = [i32, i32, i32, i32]
     lib.gd_fet_scan_device.argtypes = [vp, C.POINTER(Chrom), i32, vp, vp, vp, vp, i32, i32, C.c_double, i32,
                                        vp, vp, vp]
+    lib.gd_fet_scan_device_ex.argtypes = [vp, C.POINTER(Chrom), i32, vp, vp, vp, vp, i32, i32, C.c_double, i32, i32,
+                                          vp, vp, vp]
     lib.gd_css_scan_device.argtypes = [vp, C.POINTER(Chrom), i32, vp, vp, vp, vp, i32, i32, i32, i32, i32,
                                        vp, vp, vp]
     lib.gd_css_scan_device_ex.argtypes = [vp, C.POINTER(Chrom), i32, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32,
@@ -94,6 +103,8 @@ def _load() -> C.CDLL:
     lib.gd_last_stage_ms.argtypes = [C.POINTER(C.c_float), i32]
     lib.gd_synth_device.argtypes = [i32, i32, i32, i32, C.c_uint64, vp, vp, vp, vp, vp, vp]
     lib.gd_fet_scan_host_batch.argtypes = [C.POINTER(Chrom), i32, dp, dp, ip, ip, i32, i32, C.c_double, i32, dp, dp]
+    lib.gd_fet_scan_host_batch_ex.argtypes = [C.POINTER(Chrom), i32, dp, dp, ip, ip, i32, i32, C.c_double, i32, i32,
+                                              dp, dp]
     lib.gd_css_scan_host_batch.argtypes = [C.POINTER(Chrom), i32, dp, dp, ip, ip, i32, i32, i32, i32, i32, dp, dp]
     lib.gd_css_scan_host_batch_ex.argtypes = [C.POINTER(Chrom), i32, dp, dp, ip, ip, i32, i32, i32, i32, i32, i32, i32,
                                               dp, dp]
@@ -134,7 +145,8 @@ def _load() -> C.CDLL:
         getattr(lib, fn).restype = C.c_int
     for fn in ("gd_fet_threadcompute", "gd_fet_compute", "gd_fet_scan_host", "gd_css_threadcompute",
                "gd_css_compute", "gd_css_scan_host", "gd_css_scan_host_ex", "gd_fet_scan_device",
-               "gd_css_scan_device", "gd_css_scan_device_ex",
+               "gd_css_scan_device", "gd_css_scan_device_ex", "gd_fet_scan_host_ex", "gd_fet_scan_device_ex",
+               "gd_fet_scan_host_batch_ex", "gd_set_fet_mode", "gd_get_fet_mode",
                "gd_synth_device", "gd_device_count", "gd_window_count", "gd_last_stage_ms"):
         getattr(lib, fn).restype = C.c_int
     return lib

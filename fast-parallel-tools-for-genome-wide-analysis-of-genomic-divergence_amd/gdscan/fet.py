@@ -11,7 +11,7 @@ import ctypes as C
 
 import numpy as np
 
-from ._lib import GD_WINDOWS_SERIAL, GD_WINDOWS_THREADED, check, lib
+from ._lib import GD_FET_EXACT, GD_FET_REFERENCE, GD_WINDOWS_SERIAL, GD_WINDOWS_THREADED, check, lib
 
 _DP = C.POINTER(C.c_double)
 _IP = C.POINTER(C.c_int)
@@ -65,17 +65,35 @@ def fisher_exact_tester_serial(avals, bvals, apos, bpos, regstart, regend, wsize
          stddev)
 
 
-def scan(avals, bvals, apos, bpos, regend, wsize=2500, wstep=500, perc=0.95, seed=None, serial=False):
-    """Convenience: allocate zeroed outputs (regend//wstep) and run one chromosome."""
+def _mode(exact):
+    if exact is None:
+        return lib.gd_get_fet_mode()
+    return GD_FET_EXACT if exact else GD_FET_REFERENCE
+
+
+def set_mode(exact):
+    """Table probabilities of every call without an explicit mode, the reference-signature
+    entry points included: exact=True evaluates them from ln k! (correct for >= 68
+    individuals), False reproduces the reference's u64 binomials.  Returns the previous
+    setting (True = exact)."""
+    old = lib.gd_set_fet_mode(_mode(bool(exact)))
+    check(min(old, 0))
+    return old == GD_FET_EXACT
+
+
+def scan(avals, bvals, apos, bpos, regend, wsize=2500, wstep=500, perc=0.95, seed=None, serial=False, exact=None):
+    """Convenience: allocate zeroed outputs (regend//wstep) and run one chromosome.  exact:
+    see set_mode (None follows it)."""
     nwin = int(regend) // int(wstep)
     scores = np.zeros(nwin)
     stddev = np.zeros(nwin)
     (av, bv, ap, bp), scores, stddev = _ptrs(avals, bvals, apos, bpos, scores, stddev, "stddev")
     s = lib.gd_get_seed() if seed is None else int(seed)
-    check(lib.gd_fet_scan_host(av.ctypes.data_as(_DP), bv.ctypes.data_as(_DP), ap.ctypes.data_as(_IP),
-                               bp.ctypes.data_as(_IP), int(regend), int(wsize), int(wstep), av.shape[0],
-                               bv.shape[0], float(perc), s, GD_WINDOWS_SERIAL if serial else GD_WINDOWS_THREADED,
-                               scores.ctypes.data_as(_DP), stddev.ctypes.data_as(_DP)))
+    check(lib.gd_fet_scan_host_ex(av.ctypes.data_as(_DP), bv.ctypes.data_as(_DP), ap.ctypes.data_as(_IP),
+                                  bp.ctypes.data_as(_IP), int(regend), int(wsize), int(wstep), av.shape[0],
+                                  bv.shape[0], float(perc), _mode(exact), s,
+                                  GD_WINDOWS_SERIAL if serial else GD_WINDOWS_THREADED,
+                                  scores.ctypes.data_as(_DP), stddev.ctypes.data_as(_DP)))
     return scores, stddev
 
 

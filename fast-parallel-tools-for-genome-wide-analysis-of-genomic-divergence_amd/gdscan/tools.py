@@ -50,15 +50,17 @@ def _ptr(a, ct):
     return a.ctypes.data_as(C.POINTER(ct))
 
 
-def fisher_exact_test_snp(track_a, track_b, out_path, wsize=2500, wstep=500, percentile=0.95, chrom_lengths=None):
+def fisher_exact_test_snp(track_a, track_b, out_path, wsize=2500, wstep=500, percentile=0.95, chrom_lengths=None,
+                          exact=None):
     import ctypes as C
     names, chroms, av, bv, ap, bp, w = _batch(track_a, track_b, wstep, chrom_lengths)
     scores, stddev = np.zeros(w), np.zeros(w)
     if names:
-        check(lib.gd_fet_scan_host_batch(chroms, len(names), _ptr(av, C.c_double), _ptr(bv, C.c_double),
-                                         _ptr(ap, C.c_int), _ptr(bp, C.c_int), int(wsize), int(wstep),
-                                         float(percentile), GD_WINDOWS_THREADED, _ptr(scores, C.c_double),
-                                         _ptr(stddev, C.c_double)))
+        mode = lib.gd_get_fet_mode() if exact is None else int(bool(exact))  # GD_FET_REFERENCE / GD_FET_EXACT
+        check(lib.gd_fet_scan_host_batch_ex(chroms, len(names), _ptr(av, C.c_double), _ptr(bv, C.c_double),
+                                            _ptr(ap, C.c_int), _ptr(bp, C.c_int), int(wsize), int(wstep),
+                                            float(percentile), mode, GD_WINDOWS_THREADED,
+                                            _ptr(scores, C.c_double), _ptr(stddev, C.c_double)))
     _write(out_path, "#seqid\tstart\tscore\tstddev", names, chroms, wstep, scores, stddev)
     return names, scores, stddev
 

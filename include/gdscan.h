@@ -59,6 +59,17 @@ int gd_fet_compute(const double *avals, const double *bvals, const int *apos, co
 int gd_fet_scan_host(const double *avals, const double *bvals, const int *apos, const int *bpos, int regend,
                      int wsize, int wstep, int alen, int blen, double perc, uint64_t seed, int window_set,
                      double *scores, double *stddev);
+/* FET table probabilities.  GD_FET_REFERENCE reproduces the
+ * reference's u64 binomials (cFisher.c:245-284, 473-483), which wrap or overflow to 0 from
+ * C(68, 31) on (tables of >= 68 individuals); GD_FET_EXACT runs the same two-tailed test
+ * over hypergeometric probabilities from ln k! in double-double (~1e-13 relative). */
+#define GD_FET_REFERENCE 0
+#define GD_FET_EXACT 1
+int gd_set_fet_mode(int mode); /* mode of every call without one; returns the previous mode */
+int gd_get_fet_mode(void);
+int gd_fet_scan_host_ex(const double *avals, const double *bvals, const int *apos, const int *bpos, int regend,
+                        int wsize, int wstep, int alen, int blen, double perc, int mode, uint64_t seed,
+                        int window_set, double *scores, double *stddev);
 
 /* ---- CSS: cluster separation score (classical MDS) + Monte-Carlo p ---- */
 int gd_css_threadcompute(const double *avals, const double *bvals, const int *apos, const int *bpos, int regstart,
@@ -101,6 +112,9 @@ int gd_window_count(int regend, int wsize, int wstep, int window_set);
 int gd_fet_scan_device(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, const double *avals, const double *bvals,
                        const int32_t *apos, const int32_t *bpos, int wsize, int wstep, double perc,
                        int window_set, double *scores, double *stddev, void *hip_stream);
+int gd_fet_scan_device_ex(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, const double *avals,
+                          const double *bvals, const int32_t *apos, const int32_t *bpos, int wsize, int wstep,
+                          double perc, int mode, int window_set, double *scores, double *stddev, void *hip_stream);
 
 int gd_css_scan_device(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, const double *avals, const double *bvals,
                        const int32_t *apos, const int32_t *bpos, int wsize, int wstep, int treshold, int runs,
@@ -115,6 +129,9 @@ int gd_css_scan_device_ex(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, const
 int gd_fet_scan_host_batch(const gd_chrom *chroms, int nchrom, const double *avals, const double *bvals,
                            const int *apos, const int *bpos, int wsize, int wstep, double perc, int window_set,
                            double *scores, double *stddev);
+int gd_fet_scan_host_batch_ex(const gd_chrom *chroms, int nchrom, const double *avals, const double *bvals,
+                              const int *apos, const int *bpos, int wsize, int wstep, double perc, int mode,
+                              int window_set, double *scores, double *stddev);
 int gd_css_scan_host_batch(const gd_chrom *chroms, int nchrom, const double *avals, const double *bvals,
                            const int *apos, const int *bpos, int wsize, int wstep, int treshold, int runs,
                            int window_set, double *scores, double *p);

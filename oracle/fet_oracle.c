@@ -161,7 +161,22 @@ unsigned long orc_binomial(unsigned long n, unsigned long k) {
   return acc;
 }
 
+/* exact mode (not in the reference), the checker for
+ * gd_fet_table_p_exact: the hypergeometric probability from ln k! in long double */
+static int orc_fet_mode = 0;
+int orc_set_fet_mode(int mode) {
+  int old = orc_fet_mode;
+  orc_fet_mode = mode;
+  return old;
+}
+
 double orc_fet_p(int a, int b, int c, int d) {
+  if (orc_fet_mode) {
+    long double s = lgammal(a + b + 1.0L) + lgammal(c + d + 1.0L) + lgammal(a + c + 1.0L) + lgammal(b + d + 1.0L) -
+                    lgammal(a + 1.0L) - lgammal(b + 1.0L) - lgammal(c + 1.0L) - lgammal(d + 1.0L) -
+                    lgammal(a + b + c + d + 1.0L);
+    return (double)expl(s);
+  }
   double nom = orc_binomial(a + b, a) * orc_binomial(c + d, c);
   double den = orc_binomial(a + b + c + d, a + c);
   return nom / den;
@@ -237,7 +252,7 @@ double orc_fet(int a, int b, int c, int d) {
     orc_extreme(f);
     orc_shift(f);
     P2 = orc_fet_p(f[0], f[1], f[2], f[3]);
-    while (P2 < P0) {
+    while (P2 < (orc_fet_mode ? P0 * (1.0 - 1e-9) : P0)) { /* exact mode: ties within 1e-9 */
       P += P2;
       if (f[1] == 0 || f[2] == 0) break;
       f[0]++;

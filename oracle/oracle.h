@@ -14,6 +14,7 @@ void orc_state_words(uint64_t x, unsigned short st[3]);
 
 unsigned long orc_binomial(unsigned long n, unsigned long k);
 double orc_fet_p(int a, int b, int c, int d);
+int orc_set_fet_mode(int mode); /* 1: exact table probabilities (not in the reference) */
 double orc_fet(int a, int b, int c, int d);
 double orc_fet_score(int a, int b, int c, int d);
 void orc_fet_counts(const double *av, const double *bv, int i, int asize, int bsize, int *f);

@@ -25,3 +25,30 @@ void shim_mod(uint32_t n, const uint32_t *rs, int cnt, uint32_t *out) {
   for (int i = 0; i < cnt; ++i) out[i] = gd_randint_mod(&d, rs[i]);
 }
 int shim_pair_index(int maj, int mnr, int size) { return gd_pair_index(maj, mnr, size); }
+
+/* exact mode: gd_fet_table_p_exact over a host ln k! table */
+static double shim_lf[2][GD_BINOM_NMAX + 1];
+static int shim_lf_ready;
+static void shim_lf_init(void) {
+  if (shim_lf_ready) return;
+  for (int k = 0; k <= GD_BINOM_NMAX; ++k) {
+    const long double L = lgammal((long double)k + 1.0L);
+    shim_lf[0][k] = (double)L;
+    shim_lf[1][k] = (double)(L - (long double)shim_lf[0][k]);
+  }
+  shim_lf_ready = 1;
+}
+#define SHIM_EXACT_P(B, a, b, c, d) gd_fet_table_p_exact(shim_lf[0], shim_lf[1], (a), (b), (c), (d))
+GD_DEFINE_FET_P(shim_fet_exact_static, static, 0, SHIM_EXACT_P, GD_FET_EXACT_TIE)
+double shim_fet_p_exact(int a, int b, int c, int d) {
+  shim_lf_init();
+  return gd_fet_table_p_exact(shim_lf[0], shim_lf[1], a, b, c, d);
+}
+double shim_fet_exact(int a, int b, int c, int d) {
+  shim_lf_init();
+  return shim_fet_exact_static(a, b, c, d);
+}
+double shim_score_exact(int a, int b, int c, int d) {
+  shim_lf_init();
+  return gd_fet_score_from_p(shim_fet_exact_static(a, b, c, d));
+}
