@@ -131,11 +131,32 @@ def css_shape_run(args, lib, _lib, synth, Chrom, check, dev, stream, ctx, rank, 
     step()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    stage = _lib.last_stage_ms()  # the timed step's HIP events: [1] planes + MDS, [2] permutations
     pm = pv.cpu().numpy()
     computed = sc.cpu().numpy() != 0
-    return {"value": windows / dt, "unit": "windows/s (one GPU)", "ms": dt * 1e3, "windows": windows,
-            "config": f"{nchrom} chromosomes x {nsnp} SNPs, {pop}+{pop}, mcT={treshold}, mcR={runs}",
-            "mean_p": float(pm[computed].mean()) if computed.any() else None}
+    out = {"value": windows / dt, "unit": "windows/s (one GPU)", "ms": dt * 1e3, "windows": windows,
+           "config": f"{nchrom} chromosomes x {nsnp} SNPs, {pop}+{pop}, mcT={treshold}, mcR={runs}",
+           "mean_p": float(pm[computed].mean()) if computed.any() else None,
+           "stage_ms": {"planes_mds": stage[1], "permutations": stage[2]}}
+    if runs > 0 and computed.any():
+        # permutations run per window, from p = (hits + 1) / (run + 1): an early exit (hits =
+        # mcT) leaves p > mcT / (mcR + 1), a full run p <= mcT / (mcR + 1)
+        p = pm[computed]
+        early = p * (runs + 1) > treshold + 0.5
+        nrun = np.where(early, np.rint((treshold + 1) / p) - 1, runs)
+        perms = float(nrun.sum())
+        # (a*b + a + b) FP64 adds per permutation actually run
+        ach = perms * (pop * pop + 2 * pop) / (stage[2] * 1e-3) / 1e12
+        out["permutations"] = {
+            "total": perms, "mean_per_window": float(nrun.mean()),
+            "histogram": {"<=10": int((nrun <= 10).sum()), "11-100": int(((nrun > 10) & (nrun <= 100)).sum()),
+                          f"101-{runs - 1}": int(((nrun > 100) & (nrun < runs)).sum()),
+                          str(runs): int((nrun >= runs).sum())},
+            "per_s": perms / (stage[2] * 1e-3),
+            "roofline": {"bound": "fp64-valu / LDS", "achieved": ach, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                         "frac": ach / FP64_PEAK_TFLOPS, "kernel": "k_css_perm (HIP events)",
+                         "kernel_ms": stage[2]}}
+    return out
 
 
 def cpu_baseline(args):

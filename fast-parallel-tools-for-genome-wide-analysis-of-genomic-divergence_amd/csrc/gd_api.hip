@@ -54,7 +54,7 @@ int gd_css_launch(int mp, int drosophila, int mds, const gd_chrom_dev *d_ch, int
                   uint32_t *planes, const int32_t *lo_a, const int32_t *hi_a, const int32_t *lo_b,
                   const double *avals, const double *bvals, int64_t wtotal, int64_t max_rows_words, int treshold,
                   int runs, double *scores, double *p, double *xbuf, uint8_t *status, unsigned *flags,
-                  hipStream_t s);
+                  hipStream_t s, hipEvent_t ev_perm);
 int gd_synth_launch(int chrom, int nsnp, int asize, int bsize, uint64_t seed, const double *freq_table,
                     double *avals, double *bvals, int32_t *apos, int32_t *bpos, hipStream_t s);
 
@@ -749,14 +749,17 @@ static int css_scan_locked(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, cons
   if (perms) HIP_TRY(hipMemsetAsync(status, 0, pl.wtotal, s));
   HIP_TRY(hipEventRecord(ctx->ev[1], s));
   st = gd_css_launch(mp, drosophila, mds, d_ch, nchrom, d_pl, planes, lo_a, hi_a, lo_b, avals, bvals, pl.wtotal,
-                     max_words, treshold, runs, scores, p, xbuf, status, flags, s);
+                     max_words, treshold, runs, scores, p, xbuf, status, flags, s, ctx->ev[2]);
   if (st) return fail(st, "CSS kernel launch failed");
   HIP_TRY(hipEventRecord(ctx->ev[3], s));
   HIP_TRY(hipMemcpyAsync(ctx->h_flags, flags, 16 * sizeof(unsigned), hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
   float ms;
   if (hipEventElapsedTime(&ms, ctx->ev[0], ctx->ev[1]) == hipSuccess) g_stage_ms[GD_STAGE_MEM] = ms;
-  if (hipEventElapsedTime(&ms, ctx->ev[1], ctx->ev[3]) == hipSuccess) g_stage_ms[GD_STAGE_WINDOW] = ms;
+  /* CSS stages: MEM = population sizes + bounds, WINDOW = bit planes + MDS (+ SMACOF),
+   * GENERAL = the permutation test */
+  if (hipEventElapsedTime(&ms, ctx->ev[1], ctx->ev[2]) == hipSuccess) g_stage_ms[GD_STAGE_WINDOW] = ms;
+  if (hipEventElapsedTime(&ms, ctx->ev[2], ctx->ev[3]) == hipSuccess) g_stage_ms[GD_STAGE_GENERAL] = ms;
   if (hipEventElapsedTime(&ms, ctx->ev[0], ctx->ev[3]) == hipSuccess) g_stage_ms[GD_STAGE_TOTAL] = ms;
   return flags_to_status(ctx->h_flags[0]);
 }

@@ -126,6 +126,13 @@ __device__ __forceinline__ double lane63(double v) {
   const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), 63);
   return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
 }
+/* v of a wave-uniform lane */
+__device__ __forceinline__ double readlane_f64(double v, int lane) {
+  const uint64_t u = __builtin_bit_cast(uint64_t, v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, lane);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), lane);
+  return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
 struct OpSum {
   static __device__ __forceinline__ double id() { return 0.0; }
   static __device__ __forceinline__ double op(double x, double y) { return x + y; }
@@ -361,16 +368,23 @@ __device__ __forceinline__ void hh_step_static(double (&A)[MP], int m, int i, in
     }
   }
   const double ak1 = A[K + 1 < MP ? K + 1 : K]; /* K >= MP - 2 returned above */
-  const double sigma = block_sum<1>(xi * xi, s_red);
+  const double praw = p0 + p1;
+  /* one reduction for |x|^2 and q = r^T A r (r: row K right of the diagonal, r_{K+1} =
+   * alpha): with v = scale (r - beta e_{K+1}), v^T p = tau scale^2 (q - 2 beta (A r)_{K+1}
+   * + beta^2 A_{K+1,K+1}), so no second reduction waits on beta */
+  double sigma = xi * xi, q = ((i > K && row) ? s_row[ii] : 0.0) * praw;
+  wave_sum2(sigma, q);
+  const double pr1 = readlane_f64(praw, K + 1), a11 = readlane_f64(ak1, K + 1);
   double tau = 0.0, beta = alpha, scale = 0.0;
   if (sigma != 0.0) {
     beta = -copysign(sqrt(alpha * alpha + sigma), alpha);
-    tau = (beta - alpha) * fast_rcp(beta);
-    scale = fast_rcp(alpha - beta);
+    const double r = fast_rcp(beta * (alpha - beta)); /* 1/beta and 1/(alpha - beta) from one reciprocal */
+    tau = -(alpha - beta) * (alpha - beta) * r;
+    scale = beta * r;
   }
   const double vi = (i == K + 1) ? 1.0 : xi * scale;
-  const double pi = (i > K && row) ? (tau * scale) * fma(-beta, ak1, p0 + p1) : 0.0;
-  const double Kc = -0.5 * tau * block_sum<1>(pi * vi, s_red);
+  const double pi = (i > K && row) ? (tau * scale) * fma(-beta, ak1, praw) : 0.0;
+  const double Kc = -0.5 * tau * (tau * scale * scale) * fma(beta, fma(beta, a11, -2.0 * pr1), q);
   const double wi = fma(Kc, vi, pi);
   if (tid == 0) {
     s_e[K] = beta;
@@ -469,17 +483,27 @@ __device__ __forceinline__ void hh_step_static_g(double (&A)[MP / G], int m, int
     }
     constexpr int HK1 = (K + 1) / CP, LK1 = K + 1 - HK1 * CP;
     const double ak1 = pair_sum<G>(h == HK1 ? A[LK1] : 0.0);
-    const double sigma = block_sum<NW>(lead ? xi * xi : 0.0, s_red);
     const double praw = pair_sum<G>(p0 + p1);
+    /* one reduction for |x|^2 and r^T A r (hh_step_static); (A r)_{K+1} and A_{K+1,K+1}
+     * travel from row K+1 through the two LDS slots behind the reduction's */
+    static_assert(NW > 1, "block_sum2 synchronises the slots only across waves");
+    double sigma = lead ? xi * xi : 0.0, q = (lead && i > K && row) ? s_row[ii] * praw : 0.0;
+    if (lead && i == K + 1) {
+      s_red[2 * NW] = praw;
+      s_red[2 * NW + 1] = ak1;
+    }
+    block_sum2<NW>(sigma, q, s_red);
+    const double pr1 = s_red[2 * NW], a11 = s_red[2 * NW + 1];
     double tau = 0.0, beta = alpha, scale = 0.0;
     if (sigma != 0.0) {
       beta = -copysign(sqrt(alpha * alpha + sigma), alpha);
-      tau = (beta - alpha) * fast_rcp(beta);
-      scale = fast_rcp(alpha - beta);
+      const double r = fast_rcp(beta * (alpha - beta));
+      tau = -(alpha - beta) * (alpha - beta) * r;
+      scale = beta * r;
     }
     const double vi = (i == K + 1) ? 1.0 : xi * scale;
     const double pi = (i > K && row) ? (tau * scale) * fma(-beta, ak1, praw) : 0.0;
-    const double Kc = -0.5 * tau * block_sum<NW>(lead ? pi * vi : 0.0, s_red);
+    const double Kc = -0.5 * tau * (tau * scale * scale) * fma(beta, fma(beta, a11, -2.0 * pr1), q);
     const double wi = fma(Kc, vi, pi);
     if (tid == 0) {
       s_e[K] = beta;
@@ -543,7 +567,7 @@ __global__ void __launch_bounds__((CssShape<MP, G>::NT), CSS_MDS_WAVES(MP))
   __shared__ double s_x[2 * MP];
   __shared__ int s_tr[MP];
   __shared__ double s_lam[2];
-  __shared__ double s_red[2 * NW];
+  __shared__ double s_red[2 * NW + 2]; /* block sums; [2NW], [2NW+1]: row K+1 in a Householder step */
 
   const int tid = threadIdx.x;
   const int i = tid / G, h = tid % G; /* row, column part */
@@ -772,19 +796,36 @@ __global__ void __launch_bounds__((CssShape<MP, G>::NT), CSS_MDS_WAVES(MP))
           for (int u = 0; u < 8; ++u) ak1 = (8 * jb + u == lk1) ? A[8 * jb + u] : ak1;
         }
       }
-      const double sigma = block_sum<NW>(lead ? xi * xi : 0.0, s_red);
       const double praw = pair_sum<G>(p0 + p1);
       ak1 = pair_sum<G>(ak1);
+      /* |x|^2 and r^T A r in one reduction (hh_step_static) */
+      double sigma = lead ? xi * xi : 0.0, q = (lead && i > k && row) ? s_row[ii] * praw : 0.0;
+      double pr1, a11;
+      if constexpr (NW == 1) {
+        static_assert(G == 1, "one wave holds whole rows");
+        wave_sum2(sigma, q);
+        pr1 = readlane_f64(praw, k + 1);
+        a11 = readlane_f64(ak1, k + 1);
+      } else {
+        if (lead && i == k + 1) {
+          s_red[2 * NW] = praw;
+          s_red[2 * NW + 1] = ak1;
+        }
+        block_sum2<NW>(sigma, q, s_red);
+        pr1 = s_red[2 * NW];
+        a11 = s_red[2 * NW + 1];
+      }
       double tau = 0.0, beta = alpha, scale = 0.0;
       if (sigma != 0.0) {
         beta = -copysign(sqrt(alpha * alpha + sigma), alpha);
-        tau = (beta - alpha) * fast_rcp(beta);
-        scale = fast_rcp(alpha - beta);
+        const double r = fast_rcp(beta * (alpha - beta));
+        tau = -(alpha - beta) * (alpha - beta) * r;
+        scale = beta * r;
       }
       /* v = scale (x - beta e_{k+1}), v_{k+1} = 1;  p = tau A v */
       const double vi = (i == k + 1) ? 1.0 : xi * scale;
       const double pi = (i > k && row) ? (tau * scale) * fma(-beta, ak1, praw) : 0.0;
-      const double K = -0.5 * tau * block_sum<NW>(lead ? pi * vi : 0.0, s_red);
+      const double K = -0.5 * tau * (tau * scale * scale) * fma(beta, fma(beta, a11, -2.0 * pr1), q);
       const double wi = fma(K, vi, pi);
       if (tid == 0) {
         s_e[k] = beta;
@@ -1072,7 +1113,7 @@ int gd_css_launch(int mp, int drosophila, int mds, const gd_chrom_dev *d_ch, int
                   uint32_t *planes, const int32_t *lo_a, const int32_t *hi_a, const int32_t *lo_b,
                   const double *avals, const double *bvals, int64_t wtotal, int64_t max_rows_words, int treshold,
                   int runs, double *scores, double *p, double *xbuf, uint8_t *status, unsigned *flags,
-                  hipStream_t s) {
+                  hipStream_t s, hipEvent_t ev_perm) {
   const bool perms = runs > 0 && treshold > 0;
   const int want_x1 = (perms || mds == 2) ? 1 : 0; /* coordinates out of the classical stage */
   const char *fl = getenv("GD_CSS_FORCE_LITERAL"); /* diagnostics: per-SNP predicate for every window */
@@ -1129,6 +1170,7 @@ int gd_css_launch(int mp, int drosophila, int mds, const gd_chrom_dev *d_ch, int
                               mds, perms ? 1 : 0, force_literal, scores, p, xbuf, status, flags, s);
     if (st) return st;
   }
+  if (ev_perm && hipEventRecord(ev_perm, s) != hipSuccess) return GD_ERR_HIP; /* end of the MDS stage */
   if (perms) st = gd_css_perm_launch(mp, d_ch, nchrom, xbuf, status, wtotal, treshold, runs, p, flags + 8, s);
   return st;
 }
