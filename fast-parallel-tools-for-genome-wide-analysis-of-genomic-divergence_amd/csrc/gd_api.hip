@@ -856,7 +856,7 @@ int gd_rg_merge(const double *vals, const int32_t *seq, const int64_t *start, in
                 int64_t gap, const int64_t *seq_end, int nseq, int64_t *region_first, int64_t *region_end,
                 int64_t *nregions, int64_t *nselected, hipStream_t s);
 
-/* ctx == NULL: the calling thread's default context (device 0); stream NULL: the context's */
+/* ctx == NULL: the process-wide context of the current HIP device (hipGetDevice); stream NULL: the context's */
 template <class F>
 static int with_ctx(gd_ctx *ctx, void *hip_stream, F &&f) {
   int st = GD_OK;

@@ -275,10 +275,12 @@ static int score_at_percentile(Pool &pl, const double *v, int64_t n, double per,
   return GD_OK;
 }
 
-/* scipy.stats.cmedian(a, numbins=1000) (scipy <= 0.11, restated): histogram
- * over scipy.stats.histogram's default limits (min - s, max + s), s = (max - min) /
- * (2 (numbins - 1)); cfbin = searchsorted(cumhist, n/2.0); median = LRL + ((n/2.0 -
- * cumhist[cfbin-1]) / hist[cfbin]) * binsize, with Python's cumhist[-1] at cfbin == 0 */
+/* scipy.stats.cmedian(a, numbins=1000) (scipy 0.9-0.11, restated with its floating-point
+ * steps): scipy.stats.histogram over its default limits (smallest = min - s,
+ * max + s), s = (max - min) / (2 (numbins - 1)), binsize = bin_edges[1] - bin_edges[0];
+ * cfbin = searchsorted(cumhist, n/2.0); LRL = smallest + binsize * cfbin; median = LRL +
+ * ((n/2.0 - cumhist[cfbin-1]) / hist[cfbin]) * binsize, with Python's cumhist[-1] at
+ * cfbin == 0 */
 static int cmedian(Pool &pl, const double *v, int64_t n, double *out) {
   unsigned long long *mm;
   int st;
@@ -294,7 +296,8 @@ static int cmedian(Pool &pl, const double *v, int64_t n, double *out) {
   const double dmin = okey_value(h_mm[0]), dmax = okey_value(h_mm[1]);
   const int nb = RG_CMEDIAN_BINS;
   const double s = (dmax - dmin) / (2. * (nb - 1.));
-  double first = dmin - s, last = dmax + s;
+  const double smallest = dmin - s;
+  double first = smallest, last = dmax + s;
   if (first == last) { /* numpy.histogram widens an empty range by 0.5 each side */
     first -= 0.5;
     last += 0.5;
@@ -320,10 +323,11 @@ static int cmedian(Pool &pl, const double *v, int64_t n, double *out) {
   int cfbin = 0;
   while (cfbin < nb && (double)cum[cfbin] < half) ++cfbin;
   if (cfbin == nb) return rg_fail(GD_ERR_ARG, "cmedian: histogram lost values"); /* cannot happen */
-  const double lrl = edges[cfbin];
+  const double binsize = edges[1] - edges[0];
+  const double lrl = smallest + binsize * (double)cfbin;
   const double cfbelow = (double)cum[cfbin == 0 ? nb - 1 : cfbin - 1];
   const double freq = (double)hist[cfbin];
-  *out = lrl + ((half - cfbelow) / freq) * (edges[1] - edges[0]);
+  *out = lrl + ((half - cfbelow) / freq) * binsize;
   return GD_OK;
 }
 

@@ -141,8 +141,9 @@ int gd_css_scan_host_batch_ex(const gd_chrom *chroms, int nchrom, const double *
 
 /* ---- region filters after the scan ----
  * A track is the list of windows a tool's tabular file holds (score != 0), in file
- * order.  Array arguments may be host or device memory; ctx NULL selects the calling
- * thread's default context, hip_stream NULL the context's stream.  Blocking. */
+ * order.  Array arguments may be host or device memory; ctx NULL selects the process-wide
+ * context of the current HIP device (hipGetDevice), hip_stream NULL the context's stream.
+ * Blocking. */
 #define GD_SELECT_GE 0 /* keep vals >= thr (FET scores, CSS top-k scores) */
 #define GD_SELECT_LE 1 /* keep vals <= thr (CSS p-values) */
 /* FilterFisherScores.py:84-87: out3 = {limit, cmedian(scores), scoreatpercentile(stddev,

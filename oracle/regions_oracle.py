@@ -13,8 +13,9 @@ Restated from the reference tools (Python 2 + HyperBrowser, not importable here)
 
 Third-party arithmetic the tools call:
   scipy.stats.cmedian(a, numbins=1000) -- removed from scipy in 0.12, so it is restated
-    here from the scipy <= 0.11 source (histogram over scipy.stats.histogram's default
-    limits, then linear interpolation inside the median bin).  PARITY UNPINNED against a
+    here from the scipy 0.9-0.11 source, floating-point steps included (scipy.stats.histogram
+    over its default limits, binsize = bin_edges[1] - bin_edges[0], LRL = smallest +
+    binsize * cfbin, then linear interpolation inside the median bin).  PARITY UNPINNED against a
     live scipy: no reference fixture holds a cmedian value; the tests pin it against the
     exact median within one bin width and against a hand-computed case.
   scipy.stats.scoreatpercentile(a, per) -- restated in its scipy 0.x form
@@ -28,18 +29,28 @@ import numpy as np
 CMEDIAN_BINS = 1000
 
 
-def cmedian(a, numbins=CMEDIAN_BINS):
-    a = np.ravel(np.asarray(a, dtype=np.float64))
-    n = float(len(a))
+def histogram_limits(a, numbins):
+    """scipy.stats.histogram(a, numbins) of scipy 0.9-0.11, default limits: (hist,
+    smallest = min - s, binsize = bin_edges[1] - bin_edges[0]); numpy.histogram widens an
+    empty range internally, smallest stays min - s."""
     data_min, data_max = a.min(), a.max()
     s = (data_max - data_min) / (2.0 * (numbins - 1.0))
-    hist, bins = np.histogram(a, numbins, range=(data_min - s, data_max + s))
+    lo, hi = data_min - s, data_max + s
+    hist, bins = np.histogram(a, numbins, range=(lo, hi))
+    return np.asarray(hist, dtype=np.float64), lo, bins[1] - bins[0]
+
+
+def cmedian(a, numbins=CMEDIAN_BINS):
+    """scipy.stats.cmedian (scipy <= 0.11): LRL = smallest + binsize * cfbin."""
+    a = np.ravel(np.asarray(a, dtype=np.float64))
+    n = float(len(a))
+    hist, smallest, binsize = histogram_limits(a, numbins)
     cumhist = np.cumsum(hist)
     cfbin = int(np.searchsorted(cumhist, n / 2.0))
-    lrl = bins[cfbin]
+    lrl = smallest + binsize * cfbin
     cfbelow = cumhist[cfbin - 1]  # Python index: cumhist[-1] when cfbin == 0
     freq = float(hist[cfbin])
-    return lrl + ((n / 2.0 - cfbelow) / freq) * (bins[1] - bins[0])
+    return lrl + ((n / 2.0 - cfbelow) / freq) * binsize
 
 
 def scoreatpercentile(a, per):

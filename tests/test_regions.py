@@ -44,7 +44,18 @@ def test_cmedian_hand_case():
     a, b = 1.0, 3.0
     s = (b - a) / (2 * 999.0)
     edges = np.linspace(a - s, b + s, 1001)
-    assert ro.cmedian([a, b]) == edges[0] + ((1.0 - 2.0) / 1.0) * (edges[1] - edges[0])
+    assert ro.cmedian([a, b]) == (a - s) + ((1.0 - 2.0) / 1.0) * (edges[1] - edges[0])
+    # LRL = smallest + binsize * cfbin, not bin_edges[cfbin] (scipy 0.9-0.11 steps)
+    x = np.array([0.1, 0.7, 0.3, 0.9, 0.5])
+    s = 0.8 / (2 * 999.0)
+    hist, edges = np.histogram(x, 1000, range=(0.1 - s, 0.9 + s))
+    cfbin = int(np.searchsorted(np.cumsum(hist), 2.5))
+    bs = edges[1] - edges[0]
+    assert ro.cmedian(x) == (0.1 - s) + bs * cfbin + ((2.5 - np.cumsum(hist)[cfbin - 1]) / 1.0) * bs
+    # all values equal: numpy.histogram widens the range by 0.5 each side, smallest does not
+    e = np.linspace(1.5, 2.5, 1001)
+    bs = e[1] - e[0]
+    assert ro.cmedian(np.full(4, 2.0)) == 2.0 + bs * 500 + (2.0 / 4.0) * bs
 
 
 def test_cmedian_within_one_bin_of_median():
