@@ -43,6 +43,7 @@ __global__ void k_fet_window_general(const gd_chrom_dev *ch, int nchrom, const i
                                      int32_t *huge_list, unsigned *huge_count, double *gscratch,
                                      int64_t gscratch_n);
 int gd_fet_fast_windows_per_block();
+int gd_fet_fast_init(hipStream_t s);
 int gd_fet_window_prepare(int64_t wtotal, int32_t *slow_list, unsigned *slow_count, hipStream_t s,
                           bool *force_general);
 int gd_fet_window_fast_launch(const gd_chrom_dev *ch, int nchrom, const int32_t *blk_off, int blk_begin,
@@ -117,6 +118,7 @@ static int ctx_init(gd_ctx *c, int device) {
   hipLaunchKernelGGL(k_binom_table, dim3((GD_BINOM_ENTRIES + 255) / 256), dim3(256), 0, c->stream, c->binom);
   hipLaunchKernelGGL(k_binom_table, dim3((GD_BINOM_ENTRIES + 255) / 256), dim3(256), 0, c->stream, c->binom_exact);
   HIP_TRY(hipGetLastError());
+  if (gd_fet_fast_init(c->stream) != GD_OK) return GD_ERR_HIP;
   {
     /* behind the binomials (disjoint from the kernel's writes): the mode word, then
      * ln k! as double-double for exact mode */

@@ -23,9 +23,9 @@
  * lanes; lanes run 13 of the window's 100 replicates (the last 9).  Windows are assigned
  * to lane groups in order of n, so the windows sharing a wave run loops of similar
  * length.  The SNP scores the 32 windows touch (a contiguous row span) are staged
- * in LDS once.  Per draw: 4 VALU for the LCG step (FW_DRAW), 5 for the draw and
- * r mod n, MT (4 or 8, chosen per workgroup) for the order statistics, 1 for the
- * rejection maximum.
+ * in LDS once.  Per draw: 4 VALU for the LCG step (FW_DRAW), 2 for an order key
+ * that sorts like r mod n (fw_key: no remainder is formed inside the loop), MT (4, 5
+ * or 8, chosen per wave) for the order statistics, 1/2 for the rejection maximum.
  */
 #include <hip/hip_runtime.h>
 
@@ -109,26 +109,48 @@ __device__ __forceinline__ int fmod_n(uint32_t r, uint32_t magic, uint32_t shift
     ylo = (uint32_t)t_;                                                        \
   } while (0)
 
-/* one draw: advance, extract, reduce mod n, insert into the top-MT list */
-#define FW_DRAW(MT)                                                  \
-  do {                                                               \
-    FW_STEP();                                                       \
-    ymax = max(ymax, yhi);                                           \
-    top_insert<MT>(K, fmod_n(yhi >> 1, rd.magic, rd.shift, rd.n));   \
+/* Order key of a draw without the remainder.  The draw is r = yhi >> 1 and the
+ * sampled index r mod n; yhi = 2r + (yhi & 1) gives yhi mod 2n = 2 (r mod n) + bit,
+ * so ordering by u mod D (u = yhi, D = 2n) orders the sampled indices.  With
+ * M = ceil(2^64 / D) (Lemire's fastmod constant), L = M*u mod 2^64 equals
+ * (u mod D) 2^64/D + e with 0 <= e < u < 2^32, so key = L >> 32 grows strictly with
+ * u mod D (consecutive residues lie >= 2^32/D >= 2^23 apart) and
+ * u mod D = ((key + 1) D) >> 32.  Two VALU per draw (v_mul_hi_u32, v_mad_u64_u32)
+ * instead of the remainder's four. */
+__device__ __forceinline__ uint32_t fw_key(uint32_t u, uint32_t m_lo, uint32_t m_hi) {
+  return __umulhi(m_lo, u) + m_hi * u;
+}
+__device__ __forceinline__ int fw_key_index(uint32_t key, uint32_t D) {
+  return (int)((((uint64_t)key + 1) * D) >> 33); /* (u mod D) >> 1 = r mod n */
+}
+
+template <int MT>
+__device__ __forceinline__ void top_insert_u(uint32_t (&K)[MT], uint32_t v) {
+#pragma unroll
+  for (int i = MT - 1; i > 0; --i) K[i] = max(min(K[i - 1], K[i]), min(max(K[i - 1], K[i]), v)); /* v_med3_u32 */
+  K[0] = max(K[0], v);
+}
+
+/* one draw: advance, order key, insert into the top-MT list */
+#define FW_DRAW(MT)                          \
+  do {                                       \
+    FW_STEP();                               \
+    ymax = max(ymax, yhi);                   \
+    top_insert_u<MT>(K, fw_key(yhi, mlo, mhi)); \
   } while (0)
 
 /* lane's replicates [r0, r1) (r1 - r0 <= FW_RPT) into rep[0 .. r1-r0): y already
  * positioned at stream position r0*n.  ymax collects the high words; a draw was
  * rejected iff (ymax >> 1) > limit. */
 template <int MT>
-__device__ __forceinline__ void boot_lane(uint64_t y, int n, const gd_randint &rd, int nr, int m, int base,
-                                          double delta, const double *top, double (&rep)[FW_RPT], uint32_t &ymax,
-                                          int &worst) {
+__device__ __forceinline__ void boot_lane(uint64_t y, int n, uint64_t M, int nr, int m, int base, double delta,
+                                          const double *top, double (&rep)[FW_RPT], uint32_t &ymax, int &worst) {
   uint32_t ylo = (uint32_t)y, yhi = (uint32_t)(y >> 32);
+  const uint32_t mlo = (uint32_t)M, mhi = (uint32_t)(M >> 32), D = 2u * (uint32_t)n;
   for (int k = 0; k < nr; ++k) {
-    int K[MT];
+    uint32_t K[MT];
 #pragma unroll
-    for (int i = 0; i < MT; ++i) K[i] = -1;
+    for (int i = 0; i < MT; ++i) K[i] = 0u;
     int j = n;
     for (; j >= 8; j -= 8) {
       FW_DRAW(MT);
@@ -141,12 +163,13 @@ __device__ __forceinline__ void boot_lane(uint64_t y, int n, const gd_randint &r
       FW_DRAW(MT);
     }
     for (; j > 0; --j) FW_DRAW(MT);
-    int a = K[0], b = K[0];
+    uint32_t ka = K[0], kb = K[0];
 #pragma unroll
     for (int i = 0; i < MT; ++i) {
-      if (i == m - 1) a = K[i];
-      if (i == m - 2) b = K[i];
+      if (i == m - 1) ka = K[i];
+      if (i == m - 2) kb = K[i];
     }
+    const int a = fw_key_index(ka, D), b = fw_key_index(kb, D);
     worst = min(worst, a); /* a = t_{m-1} <= b = t_{m-2}: the lowest index read */
     const double val = gd_perc_mix(delta, top[max(a - base, 0)], top[max(b - base, 0)]);
     /* replicate k into register slot k (a select per slot keeps rep out of scratch) */
@@ -154,6 +177,15 @@ __device__ __forceinline__ void boot_lane(uint64_t y, int n, const gd_randint &r
     for (int u = 0; u < FW_RPT; ++u) rep[u] = (u == k) ? val : rep[u];
   }
 }
+
+/* Per-n constants of the draw loop, built once per device (k_fet_ntab_build):
+ * the rejection limit RAND_MAX - 2^31 mod n (cFisher.c:547-554), Lemire's
+ * M = ceil(2^64 / 2n), and the nrand48 jump to stream position 13*q*n (lane q's
+ * first replicate) as an affine map x -> mul*x + add (mod 2^48). */
+__device__ uint32_t g_ntab_limit[FW_NFAST + 1];
+__device__ uint64_t g_ntab_M[FW_NFAST + 1];
+__device__ uint64_t g_ntab_jmul[FW_NFAST + 1][FW_TPW];
+__device__ uint64_t g_ntab_jadd[FW_NFAST + 1][FW_TPW];
 
 /* Rare second pass for a window whose stream contains rejected draws
  * (random_int_nrand48 redraws while r > limit, cFisher.c:550-552): every draw
@@ -182,6 +214,19 @@ __device__ void boot_lane_rejecting(uint64_t y, int n, const gd_randint &rd, int
     const double val = gd_perc_mix(delta, top[max(a - base, 0)], top[max(b - base, 0)]);
 #pragma unroll
     for (int u = 0; u < FW_RPT; ++u) rep[u] = (u == k) ? val : rep[u];
+  }
+}
+
+__global__ void k_fet_ntab_build() {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n > FW_NFAST) return;
+  const uint32_t nn = n > 0 ? (uint32_t)n : 1u;
+  g_ntab_limit[n] = GD_RAND_MAX - (uint32_t)(0x80000000ULL % nn);
+  g_ntab_M[n] = ~0ULL / (2ull * nn) + 1;
+  for (int q = 0; q < FW_TPW; ++q) {
+    const gd_affine f = gd_lcg_jump((uint64_t)q * FW_RPT * nn);
+    g_ntab_jmul[n][q] = f.mul;
+    g_ntab_jadd[n][q] = f.add;
   }
 }
 
@@ -367,7 +412,8 @@ __global__ void __launch_bounds__(FW_WPB *FW_TPW)
   const int r0 = q * FW_RPT;
   const int r1 = min(GD_NREP, r0 + FW_RPT);
   const double delta = gd_perc_delta(n > 0 ? n : 1, perc, idx);
-  const gd_randint rd = gd_randint_make((uint32_t)(n > 0 ? n : 1));
+  const int nt = (n > 0 && n <= FW_NFAST) ? n : 1;
+  const uint32_t limit = g_ntab_limit[nt];
   uint64_t x0 = 0;
   if (fast) x0 = gd_window_state(d.seed, GD_STREAM_FET, g - d.w_base);
   double rep[FW_RPT]; /* this lane's replicates r0 .. r1-1 */
@@ -375,17 +421,18 @@ __global__ void __launch_bounds__(FW_WPB *FW_TPW)
   for (int k = 0; k < FW_RPT; ++k) rep[k] = 0.0;
   const int nr = r1 - r0;
   if (fast && sh_bad[wl] == 0) {
-    const uint64_t x = gd_affine_apply(gd_lcg_jump((uint64_t)r0 * (uint64_t)n), x0);
+    const gd_affine jump = {g_ntab_jmul[nt][q], g_ntab_jadd[nt][q]};
+    const uint64_t x = gd_affine_apply(jump, x0), M = g_ntab_M[nt];
     uint32_t ymax = 0;
     int worst = n;
     if (mmax <= 4)
-      boot_lane<4>(x << 16, n, rd, nr, m, base, delta, sh_top[wl], rep, ymax, worst);
+      boot_lane<4>(x << 16, n, M, nr, m, base, delta, sh_top[wl], rep, ymax, worst);
     else if (mmax == 5)
-      boot_lane<5>(x << 16, n, rd, nr, m, base, delta, sh_top[wl], rep, ymax, worst);
+      boot_lane<5>(x << 16, n, M, nr, m, base, delta, sh_top[wl], rep, ymax, worst);
     else
-      boot_lane<8>(x << 16, n, rd, nr, m, base, delta, sh_top[wl], rep, ymax, worst);
+      boot_lane<8>(x << 16, n, M, nr, m, base, delta, sh_top[wl], rep, ymax, worst);
     if (worst < base) atomicOr(&sh_bad[wl], FW_BAD_GENERAL);
-    if ((ymax >> 1) > rd.limit) atomicOr(&sh_bad[wl], FW_BAD_REJECT);
+    if ((ymax >> 1) > limit) atomicOr(&sh_bad[wl], FW_BAD_REJECT);
   }
   __syncthreads();
 
@@ -401,7 +448,7 @@ __global__ void __launch_bounds__(FW_WPB *FW_TPW)
     uint64_t y = gd_affine_apply(gd_lcg_jump((uint64_t)p0), x0) << 16;
     for (int64_t t = 0; t < len; ++t) {
       y = y * GD_LCG_A + FW_C16;
-      if (((uint32_t)(y >> 32) >> 1) > rd.limit) {
+      if (((uint32_t)(y >> 32) >> 1) > limit) {
         const int k = atomicAdd(&sh_nrej[wl], 1);
         if (k < FW_MAXREJ) sh_rej[wl][k] = (int)(p0 + t);
       }
@@ -424,6 +471,7 @@ __global__ void __launch_bounds__(FW_WPB *FW_TPW)
       }
       const uint64_t y = gd_affine_apply(gd_lcg_jump((uint64_t)r0 * n + c), x0) << 16;
       int worst = n;
+      const gd_randint rd = gd_randint_make((uint32_t)n);
       boot_lane_rejecting(y, n, rd, nr, m, base, delta, sh_top[wl], rep, worst);
       if (worst < base) atomicOr(&sh_bad[wl], FW_BAD_GENERAL);
     }
@@ -484,6 +532,12 @@ __global__ void k_all_windows(int32_t *list, unsigned *count, int64_t wtotal) {
 }
 
 int gd_fet_fast_windows_per_block() { return FW_WPB; }
+
+/* per-n draw constants, once per device context */
+int gd_fet_fast_init(hipStream_t s) {
+  hipLaunchKernelGGL(k_fet_ntab_build, dim3((FW_NFAST + 64) / 64), dim3(64), 0, s);
+  return hipGetLastError() == hipSuccess ? GD_OK : GD_ERR_HIP;
+}
 
 /* Resets the slow-path list; with GD_FORCE_GENERAL=1 fills it with every window and
  * tells the caller to skip the fast kernels. */

@@ -35,6 +35,16 @@ __global__ void k(unsigned *out, unsigned seed) {
       if (OP == 17) asm volatile("v_mad_u64_u32 %0, vcc, %1, %2, %0" : "+v"(u[i]) : "v"(a[i]), "v"(c) : "vcc");
       if (OP == 18) asm volatile("v_cndmask_b32 %0, %0, %1, vcc" : "+v"(a[i]) : "v"(c));
       if (OP == 19) asm volatile("v_and_b32 %0, %0, %1" : "+v"(a[i]) : "v"(c));
+      if (OP == 20) asm volatile("v_mad_u32_u24 %0, %0, %1, %1" : "+v"(a[i]) : "v"(c));
+      if (OP == 21) asm volatile("v_pk_min_u16 %0, %0, %1" : "+v"(a[i]) : "v"(c));
+      if (OP == 22) asm volatile("v_fract_f64 %0, %0" : "+v"(d[i]));
+      if (OP == 23) asm volatile("v_lshlrev_b64 %0, 3, %0" : "+v"(u[i]));
+      if (OP == 24) asm volatile("v_mad_u64_u32 %0, vcc, %1, %2, 0" : "=v"(u[i]) : "v"(a[i]), "v"(c) : "vcc");
+      if (OP == 25) asm volatile("v_bfe_u32 %0, %0, 3, 17" : "+v"(a[i]));
+      if (OP == 26) asm volatile("v_cvt_f32_u32 %0, %0" : "+v"(a[i]));
+      if (OP == 27) asm volatile("v_mul_f32 %0, %0, %1" : "+v"(a[i]) : "v"(c));
+      if (OP == 28) asm volatile("v_pk_mul_f32 %0, %0, %1" : "+v"(u[i]) : "v"(u[0]));
+      if (OP == 29) asm volatile("v_mul_lo_u32 %0, %0, %1" : "+v"(a[i]) : "s"(c));
     }
   }
   unsigned s = 0;
@@ -79,5 +89,15 @@ int main() {
   printf("v_mad_u64_u32    %.1f\n", run<17>(o));
   printf("v_cndmask_b32    %.1f\n", run<18>(o));
   printf("v_and_b32        %.1f\n", run<19>(o));
+  printf("v_mad_u32_u24    %.1f\n", run<20>(o));
+  printf("v_pk_min_u16     %.1f\n", run<21>(o));
+  printf("v_fract_f64      %.1f\n", run<22>(o));
+  printf("v_lshlrev_b64    %.1f\n", run<23>(o));
+  printf("v_mad_u64_u32 0  %.1f\n", run<24>(o));
+  printf("v_bfe_u32        %.1f\n", run<25>(o));
+  printf("v_cvt_f32_u32    %.1f\n", run<26>(o));
+  printf("v_mul_f32        %.1f\n", run<27>(o));
+  printf("v_pk_mul_f32     %.1f\n", run<28>(o));
+  printf("v_mul_lo_u32 s   %.1f\n", run<29>(o));
   return 0;
 }
