@@ -139,42 +139,51 @@ __device__ __forceinline__ void top_insert_u(uint32_t (&K)[MT], uint32_t v) {
     top_insert_u<MT>(K, fw_key(yhi, mlo, mhi)); \
   } while (0)
 
-/* lane's replicates [r0, r1) (r1 - r0 <= FW_RPT) into rep[0 .. r1-r0): y already
- * positioned at stream position r0*n.  ymax collects the high words; a draw was
- * rejected iff (ymax >> 1) > limit. */
+/* The index pair a replicate reads from the window's ranked top scores (ranks
+ * a - base and b - base, each < FW_KTOP), kept in LDS per replicate: phase C rebuilds
+ * the replicate values from them, so the draw loop holds no per-replicate registers. */
+__device__ __forceinline__ uint16_t rix_pack(int a, int b, int base) {
+  return (uint16_t)(max(a - base, 0) | (max(b - base, 0) << 8));
+}
+
+/* lane's replicates [r0, r0 + nr) (nr <= FW_RPT): y already positioned at stream
+ * position r0*n.  The draw loops run wave-uniform trip counts (scalar loop control):
+ * nlo8 = 8 floor(min n / 8) draws unrolled by 8 for every lane, then draws up to the
+ * wave's largest n with lanes past their own n masked off.  ymax collects the high
+ * words; a draw was rejected iff (ymax >> 1) > limit. */
 template <int MT>
-__device__ __forceinline__ void boot_lane(uint64_t y, int n, uint64_t M, int nr, int m, int base, double delta,
-                                          const double *top, double (&rep)[FW_RPT], uint32_t &ymax, int &worst) {
+__device__ __forceinline__ void boot_lane(uint64_t y, int n, int nlo8, int nhi, uint64_t M, int nr, int m, int base,
+                                          uint16_t *rix, uint32_t &ymax, int &worst) {
   uint32_t ylo = (uint32_t)y, yhi = (uint32_t)(y >> 32);
   const uint32_t mlo = (uint32_t)M, mhi = (uint32_t)(M >> 32), D = 2u * (uint32_t)n;
-  for (int k = 0; k < nr; ++k) {
-    uint32_t K[MT];
+  for (int k = 0; k < FW_RPT; ++k) {
+    if (k < nr) {
+      uint32_t K[MT];
 #pragma unroll
-    for (int i = 0; i < MT; ++i) K[i] = 0u;
-    int j = n;
-    for (; j >= 8; j -= 8) {
-      FW_DRAW(MT);
-      FW_DRAW(MT);
-      FW_DRAW(MT);
-      FW_DRAW(MT);
-      FW_DRAW(MT);
-      FW_DRAW(MT);
-      FW_DRAW(MT);
-      FW_DRAW(MT);
+      for (int i = 0; i < MT; ++i) K[i] = 0u;
+      int j = 0;
+      for (; j < nlo8; j += 8) {
+        FW_DRAW(MT);
+        FW_DRAW(MT);
+        FW_DRAW(MT);
+        FW_DRAW(MT);
+        FW_DRAW(MT);
+        FW_DRAW(MT);
+        FW_DRAW(MT);
+        FW_DRAW(MT);
+      }
+      for (; j < nhi; ++j)
+        if (j < n) FW_DRAW(MT);
+      uint32_t ka = K[0], kb = K[0];
+#pragma unroll
+      for (int i = 0; i < MT; ++i) {
+        if (i == m - 1) ka = K[i];
+        if (i == m - 2) kb = K[i];
+      }
+      const int a = fw_key_index(ka, D), b = fw_key_index(kb, D);
+      worst = min(worst, a); /* a = t_{m-1} <= b = t_{m-2}: the lowest index read */
+      rix[k] = rix_pack(a, b, base);
     }
-    for (; j > 0; --j) FW_DRAW(MT);
-    uint32_t ka = K[0], kb = K[0];
-#pragma unroll
-    for (int i = 0; i < MT; ++i) {
-      if (i == m - 1) ka = K[i];
-      if (i == m - 2) kb = K[i];
-    }
-    const int a = fw_key_index(ka, D), b = fw_key_index(kb, D);
-    worst = min(worst, a); /* a = t_{m-1} <= b = t_{m-2}: the lowest index read */
-    const double val = gd_perc_mix(delta, top[max(a - base, 0)], top[max(b - base, 0)]);
-    /* replicate k into register slot k (a select per slot keeps rep out of scratch) */
-#pragma unroll
-    for (int u = 0; u < FW_RPT; ++u) rep[u] = (u == k) ? val : rep[u];
   }
 }
 
@@ -191,7 +200,7 @@ __device__ uint64_t g_ntab_jadd[FW_NFAST + 1][FW_TPW];
  * (random_int_nrand48 redraws while r > limit, cFisher.c:550-552): every draw
  * loops until accepted, starting from the lane's corrected stream position. */
 __device__ void boot_lane_rejecting(uint64_t y, int n, const gd_randint &rd, int nr, int m, int base,
-                                    double delta, const double *top, double (&rep)[FW_RPT], int &worst) {
+                                    uint16_t *rix, int &worst) {
   for (int k = 0; k < nr; ++k) {
     int K[8];
 #pragma unroll
@@ -211,9 +220,7 @@ __device__ void boot_lane_rejecting(uint64_t y, int n, const gd_randint &rd, int
       if (i == m - 2) b = K[i];
     }
     worst = min(worst, a);
-    const double val = gd_perc_mix(delta, top[max(a - base, 0)], top[max(b - base, 0)]);
-#pragma unroll
-    for (int u = 0; u < FW_RPT; ++u) rep[u] = (u == k) ? val : rep[u];
+    rix[k] = rix_pack(a, b, base);
   }
 }
 
@@ -257,6 +264,7 @@ __global__ void __launch_bounds__(FW_WPB *FW_TPW)
   __shared__ int64_t sh_row[FW_WPB]; /* snp_score index of the window's first row; -1: not fast */
   __shared__ int sh_n[FW_WPB], sh_key[FW_WPB], sh_bad[FW_WPB], sh_slot[FW_WPB], sh_nrej[FW_WPB];
   __shared__ int sh_rej[FW_WPB][FW_MAXREJ];
+  __shared__ uint16_t sh_rix[FW_WPB][FW_TPW * FW_RPT]; /* per replicate: rank pair read (rix_pack) */
   __shared__ unsigned long long sh_lo, sh_hi;
 
   if (*flags & (GD_FLAG_UNSORTED_A | GD_FLAG_UNSORTED_B | GD_FLAG_BAD_SIZE)) return;
@@ -405,10 +413,18 @@ __global__ void __launch_bounds__(FW_WPB *FW_TPW)
 
   FW_PROF(1);
   /* ---- B. bootstrap replicates: lane q runs replicates [13q, 13q+13) ---- */
-  /* order statistics tracked: the largest m among this wave's fast windows */
-  int mmax = (fast && sh_bad[wl] == 0) ? m : 0;
+  /* wave-uniform loop shape: the largest m (order statistics tracked) and the
+   * smallest / largest n among this wave's bootstrapped windows */
+  const bool boot = fast && sh_bad[wl] == 0;
+  int mmax = boot ? m : 0, nmin = boot ? n : 1 << 30, nmax = boot ? n : 0;
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) mmax = max(mmax, __shfl_xor(mmax, o));
+  for (int o = 32; o > 0; o >>= 1) {
+    mmax = max(mmax, __shfl_xor(mmax, o));
+    nmin = min(nmin, __shfl_xor(nmin, o));
+    nmax = max(nmax, __shfl_xor(nmax, o));
+  }
+  mmax = __builtin_amdgcn_readfirstlane(mmax);
+  const int nlo8 = __builtin_amdgcn_readfirstlane(nmin) & ~7, nhi = __builtin_amdgcn_readfirstlane(nmax);
   const int r0 = q * FW_RPT;
   const int r1 = min(GD_NREP, r0 + FW_RPT);
   const double delta = gd_perc_delta(n > 0 ? n : 1, perc, idx);
@@ -416,21 +432,23 @@ __global__ void __launch_bounds__(FW_WPB *FW_TPW)
   const uint32_t limit = g_ntab_limit[nt];
   uint64_t x0 = 0;
   if (fast) x0 = gd_window_state(d.seed, GD_STREAM_FET, g - d.w_base);
-  double rep[FW_RPT]; /* this lane's replicates r0 .. r1-1 */
-#pragma unroll
-  for (int k = 0; k < FW_RPT; ++k) rep[k] = 0.0;
+#ifdef GD_FET_NODRAW
+  const int nr = 0; /* diagnostics: setup cost only */
+#else
   const int nr = r1 - r0;
-  if (fast && sh_bad[wl] == 0) {
+#endif
+  uint16_t *rix = sh_rix[wl] + r0;
+  if (boot) {
     const gd_affine jump = {g_ntab_jmul[nt][q], g_ntab_jadd[nt][q]};
     const uint64_t x = gd_affine_apply(jump, x0), M = g_ntab_M[nt];
     uint32_t ymax = 0;
     int worst = n;
     if (mmax <= 4)
-      boot_lane<4>(x << 16, n, M, nr, m, base, delta, sh_top[wl], rep, ymax, worst);
+      boot_lane<4>(x << 16, n, nlo8, nhi, M, nr, m, base, rix, ymax, worst);
     else if (mmax == 5)
-      boot_lane<5>(x << 16, n, M, nr, m, base, delta, sh_top[wl], rep, ymax, worst);
+      boot_lane<5>(x << 16, n, nlo8, nhi, M, nr, m, base, rix, ymax, worst);
     else
-      boot_lane<8>(x << 16, n, M, nr, m, base, delta, sh_top[wl], rep, ymax, worst);
+      boot_lane<8>(x << 16, n, nlo8, nhi, M, nr, m, base, rix, ymax, worst);
     if (worst < base) atomicOr(&sh_bad[wl], FW_BAD_GENERAL);
     if ((ymax >> 1) > limit) atomicOr(&sh_bad[wl], FW_BAD_REJECT);
   }
@@ -472,7 +490,7 @@ __global__ void __launch_bounds__(FW_WPB *FW_TPW)
       const uint64_t y = gd_affine_apply(gd_lcg_jump((uint64_t)r0 * n + c), x0) << 16;
       int worst = n;
       const gd_randint rd = gd_randint_make((uint32_t)n);
-      boot_lane_rejecting(y, n, rd, nr, m, base, delta, sh_top[wl], rep, worst);
+      boot_lane_rejecting(y, n, rd, nr, m, base, rix, worst);
       if (worst < base) atomicOr(&sh_bad[wl], FW_BAD_GENERAL);
     }
   }
@@ -484,6 +502,15 @@ __global__ void __launch_bounds__(FW_WPB *FW_TPW)
    * walks down the window's 8 lanes (lane q holds replicates 13q ..), handed from
    * lane to lane with a DPP row shift */
   const bool live = fast && !(sh_bad[wl] & FW_BAD_GENERAL);
+  double rep[FW_RPT]; /* this lane's replicates r0 .. r1-1, rebuilt from their rank pairs */
+#pragma unroll
+  for (int k = 0; k < FW_RPT; ++k) {
+    rep[k] = 0.0;
+    if (live && k < nr) {
+      const unsigned w = rix[k];
+      rep[k] = gd_perc_mix(delta, sh_top[wl][w & 255u], sh_top[wl][w >> 8]);
+    }
+  }
   double sum = 0.0;
 #pragma unroll
   for (int step = FW_TPW - 1; step >= 0; --step) {
