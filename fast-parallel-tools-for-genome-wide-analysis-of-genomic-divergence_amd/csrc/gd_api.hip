@@ -30,7 +30,7 @@ __global__ void k_popsize(gd_chrom_dev *ch, const int32_t *apos, const int32_t *
 __global__ void k_bounds(const gd_chrom_dev *ch, const int32_t *apos, const int32_t *bpos, int wsize, int wstep,
                          int32_t *lo_a, int32_t *hi_a, int32_t *lo_b, unsigned *flags);
 __global__ void k_snp_fet(const gd_chrom_dev *ch, const double *avals, const double *bvals, const uint64_t *binom,
-                          const int *lut_hdr, const double *lut, double *snp_score);
+                          const int *lut_hdr, const double *lut, double *snp_score, int skip_table_held);
 __global__ void k_fet_lut_build(const gd_chrom_dev *ch, const uint64_t *binom, const int *hdr, double *lut,
                                 int64_t cap);
 __global__ void k_fet_lut_publish(const gd_chrom_dev *ch, const uint64_t *binom, int *hdr, int64_t cap);
@@ -39,7 +39,8 @@ __global__ void k_fet_window_general(const gd_chrom_dev *ch, int nchrom, const i
                                      const unsigned *wlist_count, int64_t wtotal, const int32_t *lo_a,
                                      const int32_t *hi_a, const int32_t *lo_b, const double *avals,
                                      const double *bvals, const double *snp_score, const uint64_t *binom,
-                                     double perc, double *scores, double *stddev, unsigned *flags,
+                                     const int *lut_hdr, const double *lut, double perc, double *scores,
+                                     double *stddev, unsigned *flags,
                                      int32_t *huge_list, unsigned *huge_count, double *gscratch,
                                      int64_t gscratch_n);
 int gd_fet_fast_windows_per_block();
@@ -48,8 +49,10 @@ int gd_fet_window_prepare(int64_t wtotal, int32_t *slow_list, unsigned *slow_cou
                           bool *force_general);
 int gd_fet_window_fast_launch(const gd_chrom_dev *ch, int nchrom, const int32_t *blk_off, int blk_begin,
                               int blk_count, const int32_t *lo_a, const int32_t *hi_a, const int32_t *lo_b,
-                              const double *snp_score, double perc, double *scores, double *stddev,
-                              unsigned *flags, int32_t *slow_list, unsigned *slow_count, hipStream_t s);
+                              const double *snp_score, const double *avals, const double *bvals,
+                              const uint64_t *binom, const int *lut_hdr, const double *lut, int fused, double perc,
+                              double *scores, double *stddev, unsigned *flags, int32_t *slow_list,
+                              unsigned *slow_count, hipStream_t s);
 int gd_css_tier(int m);
 int gd_css_launch(int mp, int drosophila, int mds, const gd_chrom_dev *d_ch, int nchrom, const gd_css_planes *d_pl,
                   uint32_t *planes, const int32_t *lo_a, const int32_t *hi_a, const int32_t *lo_b,
@@ -352,8 +355,14 @@ static int fet_scan_locked(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, cons
                      (int64_t)GD_LUT_CAP);
   hipLaunchKernelGGL(k_fet_lut_publish, dim3(1), dim3(1), 0, sm, d_ch, binom, ctx->lut_hdr, (int64_t)GD_LUT_CAP);
 
-  int G = std::min(nchrom, GD_MAX_GROUPS);
-  if (const char *eg = getenv("GD_GROUPS")) G = std::max(1, std::min(G, atoi(eg))); /* diagnostics */
+  /* fused (default): wherever the score table holds a chromosome's sizes, the window
+   * kernel scores its own span rows from the genotype values and the per-SNP pass
+   * (k_snp_fet) exits at once, so the only full pass is k_bounds; GD_FET_UNFUSED=1
+   * restores the per-SNP pass feeding the window kernel through snp_score */
+  const char *uf = getenv("GD_FET_UNFUSED");
+  const bool fused = !(uf && uf[0] == '1');
+  int G = std::min(nchrom, GD_DEFAULT_GROUPS);
+  if (const char *eg = getenv("GD_GROUPS")) G = std::max(1, std::min(std::min(nchrom, GD_MAX_GROUPS), atoi(eg))); /* diagnostics */
   std::vector<int> cuts(G + 1);
   for (int g = 0; g <= G; ++g) cuts[g] = (int)((int64_t)nchrom * g / G);
   for (int g = 0; g < G; ++g) {
@@ -369,7 +378,7 @@ static int fet_scan_locked(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, cons
                        hi_a, lo_b, flags);
     const unsigned gxs = (unsigned)std::min<int64_t>((amax + 255) / 256, std::max(1, 8192 / nc));
     hipLaunchKernelGGL(k_snp_fet, dim3(gxs, nc), dim3(256), 0, sm, d_ch + c0, avals, bvals, binom,
-                       ctx->lut_hdr, ctx->lut, snp);
+                       ctx->lut_hdr, ctx->lut, snp, fused ? 1 : 0);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(ctx->gev[g], sm));
   }
@@ -378,7 +387,8 @@ static int fet_scan_locked(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, cons
     const int c0 = cuts[g], c1 = cuts[g + 1];
     HIP_TRY(hipStreamWaitEvent(s2, ctx->gev[g], 0));
     st = gd_fet_window_fast_launch(d_ch, nchrom, d_blk, blk_off[c0], blk_off[c1] - blk_off[c0], lo_a, hi_a, lo_b,
-                                   snp, perc, scores, stddev, flags, list, list_count, s2);
+                                   snp, avals, bvals, binom, ctx->lut_hdr, ctx->lut, fused ? 1 : 0, perc, scores,
+                                   stddev, flags, list, list_count, s2);
     if (st) return fail(st, "fast window kernel launch failed");
   }
   HIP_TRY(hipEventRecord(ctx->ev[2], s2));
@@ -388,7 +398,8 @@ static int fet_scan_locked(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, cons
     /* windows the fast path declined: literal one-workgroup-per-window path */
     const unsigned gx = (unsigned)std::min<int64_t>(pl.wtotal, 4096);
     hipLaunchKernelGGL((k_fet_window_general<64, false>), dim3(gx), dim3(64), 0, s, d_ch, nchrom, list,
-                       list_count, pl.wtotal, lo_a, hi_a, lo_b, avals, bvals, snp, binom, perc, scores,
+                       list_count, pl.wtotal, lo_a, hi_a, lo_b, avals, bvals, snp, binom,
+                       fused ? ctx->lut_hdr : (const int *)nullptr, ctx->lut, perc, scores,
                        stddev, flags, huge, huge_count, (double *)nullptr, (int64_t)0);
   }
   HIP_TRY(hipGetLastError());
@@ -411,7 +422,8 @@ static int fet_scan_locked(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, cons
       ctx->gscratch_cap = per * slots;
     }
     hipLaunchKernelGGL((k_fet_window_general<256, true>), dim3(slots), dim3(256), 0, s, d_ch, nchrom, huge,
-                       huge_count, (int64_t)0, lo_a, hi_a, lo_b, avals, bvals, snp, binom, perc, scores,
+                       huge_count, (int64_t)0, lo_a, hi_a, lo_b, avals, bvals, snp, binom,
+                       fused ? ctx->lut_hdr : (const int *)nullptr, ctx->lut, perc, scores,
                        stddev, flags, (int32_t *)nullptr, (unsigned *)nullptr, ctx->gscratch, per);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipMemcpyAsync(ctx->h_flags, flags, 16 * sizeof(unsigned), hipMemcpyDeviceToHost, s));

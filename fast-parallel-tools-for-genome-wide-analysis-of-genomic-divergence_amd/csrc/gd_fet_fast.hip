@@ -9,7 +9,8 @@
  * t_1 >= ... are the sampled indices in descending order and m = n - idx
  * (m ~ 3-4 at perc 0.95).  Each lane keeps the MT largest indices of its
  * replicate in registers (one v_med3_i32 per slot per draw); no sort, no histogram.
- * The window's top-KTOP scores are ranked once into LDS.
+ * The window's top-KTOP scores are ranked once into LDS (a bitonic sort across
+ * the window's 8 lanes for n <= 64).
  *
  * Parallel RNG.  nrand48 is x -> (a x + c) mod 2^48; lane q of a window starts
  * its replicates at stream position 13*q*n via an affine jump (gd_lcg_jump), so
@@ -34,14 +35,19 @@
 
 #include "../../include/gdscan.h"
 #include "gd_common.h"
+#include "gd_fet_rows.h"
 #include "gd_internal.h"
 
-#define FW_WPB 32    /* windows per workgroup */
+#ifndef FW_WPB
+#define FW_WPB 32    /* windows per workgroup (sorted by (m, n) into waves of 8; 64 measured slower) */
+#endif
 #define FW_TPW 8     /* lanes per window (10 and 4 measured 35% / 22% slower) */
 #define FW_RPT 13    /* replicates per lane (8*13 >= 100; the last lane runs 9) */
 #define FW_KTOP 24   /* ranked top scores kept per window (P(needing more) < 1e-9 per replicate) */
 #define FW_NFAST 256 /* largest window handled here */
+#ifndef FW_SPAN
 #define FW_SPAN 1024 /* staged SNP rows per workgroup (32 windows need ~400 at 50 SNPs/window) */
+#endif
 #define FW_MAXREJ 8  /* rejected draws tracked per window before giving up */
 
 #define FW_BAD_GENERAL 1 /* hand the window to the literal general path */
@@ -150,10 +156,11 @@ __device__ __forceinline__ uint16_t rix_pack(int a, int b, int base) {
  * position r0*n.  The draw loops run wave-uniform trip counts (scalar loop control):
  * nlo8 = 8 floor(min n / 8) draws unrolled by 8 for every lane, then draws up to the
  * wave's largest n with lanes past their own n masked off.  ymax collects the high
- * words; a draw was rejected iff (ymax >> 1) > limit. */
+ * words; a draw was rejected iff (ymax >> 1) > limit.  muni: the wave's common m
+ * (scalar), 0 when its windows differ. */
 template <int MT>
-__device__ __forceinline__ void boot_lane(uint64_t y, int n, int nlo8, int nhi, uint64_t M, int nr, int m, int base,
-                                          uint16_t *rix, uint32_t &ymax, int &worst) {
+__device__ __forceinline__ void boot_lane(uint64_t y, int n, int nlo8, int nhi, uint64_t M, int nr, int m, int muni,
+                                          int base, uint16_t *rix, uint32_t &ymax, int &worst) {
   uint32_t ylo = (uint32_t)y, yhi = (uint32_t)(y >> 32);
   const uint32_t mlo = (uint32_t)M, mhi = (uint32_t)(M >> 32), D = 2u * (uint32_t)n;
   for (int k = 0; k < FW_RPT; ++k) {
@@ -175,10 +182,20 @@ __device__ __forceinline__ void boot_lane(uint64_t y, int n, int nlo8, int nhi, 
       for (; j < nhi; ++j)
         if (j < n) FW_DRAW(MT);
       uint32_t ka = K[0], kb = K[0];
+      if (muni > 0) {
+        /* the wave shares one m (the usual case): static register picks */
 #pragma unroll
-      for (int i = 0; i < MT; ++i) {
-        if (i == m - 1) ka = K[i];
-        if (i == m - 2) kb = K[i];
+        for (int i = 1; i < MT; ++i)
+          if (i == muni - 1) {
+            ka = K[i];
+            kb = K[i - 1];
+          }
+      } else {
+#pragma unroll
+        for (int i = 0; i < MT; ++i) {
+          if (i == m - 1) ka = K[i];
+          if (i == m - 2) kb = K[i];
+        }
       }
       const int a = fw_key_index(ka, D), b = fw_key_index(kb, D);
       worst = min(worst, a); /* a = t_{m-1} <= b = t_{m-2}: the lowest index read */
@@ -254,17 +271,115 @@ __device__ __forceinline__ double group8_max(double v) {
   return v;
 }
 
+/* Per-SNP scores of chromosome rows [r0, r0 + nrows) into dst[0 .. nrows): tiles of
+ * R rows; the workgroup's waves stream each tile's A and B values (four 16-byte
+ * loads per lane in flight), ballot them into "== 3" / "== -3" masks in LDS, then
+ * one thread per row counts its popcounts and looks the score table up (the caller
+ * checked that the table holds this chromosome's sizes). */
+__device__ void fw_stage_scores(const gd_chrom_dev &d, int r0, int nrows, const double *avals, const double *bvals,
+                                const double *lut, uint64_t (*m)[2][SF_MAXCH][2], double *dst) {
+  constexpr int NT = FW_WPB * FW_TPW, NW = NT / 64;
+  const int asize = d.asize, bsize = d.bsize;
+  const int lut_nb = (bsize + 1) * (bsize + 2) / 2;
+  const int R = min(NT, ((SF_MAXCH - 2) * 128) / max(max(asize, bsize), 1));
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int t0 = 0; t0 < nrows; t0 += R) {
+    const int rows = min(R, nrows - t0);
+    int rel0[2];
+#pragma unroll
+    for (int pop = 0; pop < 2; ++pop) {
+      const int size = pop ? bsize : asize;
+      const double *vals = pop ? bvals : avals;
+      const int64_t start = (pop ? d.b_off : d.a_off) + (int64_t)(r0 + t0) * size;
+      const int64_t stop = start + (int64_t)rows * size;
+      const int64_t gb = start & ~(int64_t)1; /* 16-byte aligned element */
+      rel0[pop] = (int)(start - gb);
+      const int nch = (int)((stop - gb + 127) >> 7);
+      for (int k0 = wave; k0 < nch; k0 += 4 * NW) {
+        double2 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int64_t e = gb + ((int64_t)(k0 + u * NW) << 7) + 2 * lane;
+          v[u].x = 0.0;
+          v[u].y = 0.0;
+          if (e + 1 < stop)
+            v[u] = *reinterpret_cast<const double2 *>(vals + e);
+          else if (e < stop)
+            v[u].x = vals[e];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int k = k0 + u * NW;
+          const uint64_t ja = __ballot(v[u].x == 3.0), jb = __ballot(v[u].y == 3.0);
+          const uint64_t na = __ballot(v[u].x == -3.0), nb = __ballot(v[u].y == -3.0);
+          if (lane == 0 && k < nch) {
+            m[pop][0][k][0] = ja;
+            m[pop][0][k][1] = jb;
+            m[pop][1][k][0] = na;
+            m[pop][1][k][1] = nb;
+          }
+        }
+      }
+    }
+    __syncthreads();
+    for (int r = threadIdx.x; r < rows; r += NT) {
+      const int sa = rel0[0] + r * asize, sb = rel0[1] + r * bsize;
+      const int f0 = count_range(m[0][0], sa, sa + asize);
+      const int f1 = count_range(m[0][1], sa, sa + asize);
+      const int f2 = count_range(m[1][0], sb, sb + bsize);
+      const int f3 = count_range(m[1][1], sb, sb + bsize);
+      dst[t0 + r] = lut[(int64_t)gd_pair_index(f0, f1, asize) * lut_nb + gd_pair_index(f2, f3, bsize)];
+    }
+    __syncthreads();
+  }
+}
+
+/* one compare-exchange step of the lane-group bitonic sort: every register r meets
+ * the partner lane's register (MIRROR ? 7 - r : r); the upper lane keeps the larger */
+template <int CTRL, bool MIRROR>
+__device__ __forceinline__ void fw_cross(double (&v)[8], bool upper) {
+  double p[8];
+#pragma unroll
+  for (int r = 0; r < 8; ++r) p[r] = dpp_f64<CTRL>(v[MIRROR ? 7 - r : r]);
+#pragma unroll
+  for (int r = 0; r < 8; ++r) v[r] = ((v[r] > p[r]) == upper) ? v[r] : p[r];
+}
+
+/* in-lane half-cleaners (register distances 4, 2, 1): a bitonic 8 -> descending */
+__device__ __forceinline__ void fw_clean8(double (&v)[8]) {
+#define FW_CX2(a, b)                       \
+  do {                                     \
+    const double hi_ = fmax(v[a], v[b]);   \
+    v[b] = fmin(v[a], v[b]);               \
+    v[a] = hi_;                            \
+  } while (0)
+  FW_CX2(0, 4); FW_CX2(1, 5); FW_CX2(2, 6); FW_CX2(3, 7);
+  FW_CX2(0, 2); FW_CX2(1, 3); FW_CX2(4, 6); FW_CX2(5, 7);
+  FW_CX2(0, 1); FW_CX2(2, 3); FW_CX2(4, 5); FW_CX2(6, 7);
+#undef FW_CX2
+}
+
 __global__ void __launch_bounds__(FW_WPB *FW_TPW)
     k_fet_window_fast(const gd_chrom_dev *ch, int nchrom, const int32_t *blk_off, int blk_base,
                       const int32_t *lo_a, const int32_t *hi_a, const int32_t *lo_b, const double *snp_score,
-                      double perc, double *scores, double *stddev, const unsigned *flags, int32_t *slow_list,
-                      unsigned *slow_count) {
+                      const double *avals, const double *bvals, const uint64_t *binom, const int *lut_hdr,
+                      const double *lut, int fused, double perc, double *scores, double *stddev,
+                      const unsigned *flags, int32_t *slow_list, unsigned *slow_count) {
   __shared__ double sh_span[FW_SPAN];
-  __shared__ double sh_top[FW_WPB][FW_KTOP];
+  /* the ballot masks of the span staging (fused mode) share LDS with the ranked top
+   * scores and the replicate rank pairs, which are written only after it */
+  __shared__ union {
+    struct {
+      double top[FW_WPB][FW_KTOP];
+      uint16_t rix[FW_WPB][FW_TPW * FW_RPT]; /* per replicate: rank pair read (rix_pack) */
+    } b;
+    uint64_t m[2][2][SF_MAXCH][2]; /* [pop][== 3 / == -3][chunk][even / odd element] */
+  } sh_u;
+  double(&sh_top)[FW_WPB][FW_KTOP] = sh_u.b.top;
+  uint16_t(&sh_rix)[FW_WPB][FW_TPW * FW_RPT] = sh_u.b.rix;
   __shared__ int64_t sh_row[FW_WPB]; /* snp_score index of the window's first row; -1: not fast */
   __shared__ int sh_n[FW_WPB], sh_key[FW_WPB], sh_bad[FW_WPB], sh_slot[FW_WPB], sh_nrej[FW_WPB];
   __shared__ int sh_rej[FW_WPB][FW_MAXREJ];
-  __shared__ uint16_t sh_rix[FW_WPB][FW_TPW * FW_RPT]; /* per replicate: rank pair read (rix_pack) */
   __shared__ unsigned long long sh_lo, sh_hi;
 
   if (*flags & (GD_FLAG_UNSORTED_A | GD_FLAG_UNSORTED_B | GD_FLAG_BAD_SIZE)) return;
@@ -337,7 +452,14 @@ __global__ void __launch_bounds__(FW_WPB *FW_TPW)
   }
   const int64_t span0 = (int64_t)sh_lo;
   const int spanlen = sh_hi > sh_lo ? (int)(sh_hi - sh_lo) : 0;
-  for (int i = tid; i < spanlen; i += FW_WPB * FW_TPW) sh_span[i] = snp_score[span0 + i];
+  if (fused && gd_lut_holds(lut_hdr, d.asize, d.bsize, binom)) {
+    /* fused: the span rows' -log10 p from the genotype values (fetcount + the score
+     * table, as k_snp_fet) -- the values are read here, once per workgroup */
+    fw_stage_scores(d, (int)(span0 - d.a_off), spanlen, avals, bvals, lut, sh_u.m, sh_span);
+  } else {
+    /* k_snp_fet scored the rows (unfused mode, or sizes the table does not hold) */
+    for (int i = tid; i < spanlen; i += FW_WPB * FW_TPW) sh_span[i] = snp_score[span0 + i];
+  }
   __syncthreads();
 
   FW_PROF(0);
@@ -355,8 +477,8 @@ __global__ void __launch_bounds__(FW_WPB *FW_TPW)
     const double *S = sh_span + (sh_row[wl] - span0);
     int nan = 0;
     if (n <= FW_TPW * 8) {
-      /* each lane sorts its <= 8 scores (S[q], S[q+8], ...) descending in registers,
-       * stages them in LDS, and the 8 lanes merge: KTOP rounds of an 8-way max */
+      /* each lane sorts its <= 8 scores (S[q], S[q+8], ...) descending in registers
+       * (padding -inf), then the 8 lanes merge their runs */
       double v[8];
       int cnt = 0;
 #pragma unroll
@@ -380,20 +502,23 @@ __global__ void __launch_bounds__(FW_WPB *FW_TPW)
       FW_CX(2, 4); FW_CX(3, 5);
       FW_CX(1, 2); FW_CX(3, 4); FW_CX(5, 6);
 #undef FW_CX
-      /* merge: each round the group's largest head is popped by its lowest lane
-       * (the lane's sorted list shifts up; exhausted slots read -inf) */
-      const int gbase = (threadIdx.x & 63) & ~7; /* first lane of this group in the wave */
-      for (int t = 0; t < ktop; ++t) {
-        const double c = v[0];
-        const double cmax = group8_max(c);
-        const uint64_t hit = __ballot(c == cmax);
-        const unsigned grp = (unsigned)(hit >> gbase) & 0xFFu;
-        if (q == __builtin_ctz(grp)) {
+      /* bitonic merges across the 8 lanes (element e = 8q + r, descending): blocks of
+       * 8 -> 16 -> 32 -> 64.  Each merge starts with a mirror step (lane q against the
+       * block's mirror lane, register r against 7 - r), then half-cleaners at lane
+       * distances 2, 1 (DPP) and register distances 4, 2, 1 */
+      fw_cross<0xB1, true>(v, (q & 1) == 0);  /* 16: mirror in lane pairs */
+      fw_clean8(v);
+      fw_cross<0x1B, true>(v, (q & 2) == 0);  /* 32: mirror in quads */
+      fw_cross<0xB1, false>(v, (q & 1) == 0); /*     lane distance 1 */
+      fw_clean8(v);
+      fw_cross<0x141, true>(v, (q & 4) == 0); /* 64: mirror in the 8 lanes */
+      fw_cross<0x4E, false>(v, (q & 2) == 0); /*     lane distance 2 */
+      fw_cross<0xB1, false>(v, (q & 1) == 0); /*     lane distance 1 */
+      fw_clean8(v);
 #pragma unroll
-          for (int u = 0; u < 7; ++u) v[u] = v[u + 1];
-          v[7] = -__builtin_inf();
-        }
-        if (q == 0) sh_top[wl][ktop - 1 - t] = cmax;
+      for (int r = 0; r < 8; ++r) {
+        const int e = FW_TPW * q + r; /* ascending rank n - 1 - e */
+        if (e < ktop) sh_top[wl][ktop - 1 - e] = v[r];
       }
       (void)cnt;
     } else {
@@ -416,14 +541,16 @@ __global__ void __launch_bounds__(FW_WPB *FW_TPW)
   /* wave-uniform loop shape: the largest m (order statistics tracked) and the
    * smallest / largest n among this wave's bootstrapped windows */
   const bool boot = fast && sh_bad[wl] == 0;
-  int mmax = boot ? m : 0, nmin = boot ? n : 1 << 30, nmax = boot ? n : 0;
+  int mmax = boot ? m : 0, mmin = boot ? m : 1 << 30, nmin = boot ? n : 1 << 30, nmax = boot ? n : 0;
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     mmax = max(mmax, __shfl_xor(mmax, o));
+    mmin = min(mmin, __shfl_xor(mmin, o));
     nmin = min(nmin, __shfl_xor(nmin, o));
     nmax = max(nmax, __shfl_xor(nmax, o));
   }
   mmax = __builtin_amdgcn_readfirstlane(mmax);
+  const int muni = __builtin_amdgcn_readfirstlane(mmin) == mmax ? mmax : 0;
   const int nlo8 = __builtin_amdgcn_readfirstlane(nmin) & ~7, nhi = __builtin_amdgcn_readfirstlane(nmax);
   const int r0 = q * FW_RPT;
   const int r1 = min(GD_NREP, r0 + FW_RPT);
@@ -444,11 +571,11 @@ __global__ void __launch_bounds__(FW_WPB *FW_TPW)
     uint32_t ymax = 0;
     int worst = n;
     if (mmax <= 4)
-      boot_lane<4>(x << 16, n, nlo8, nhi, M, nr, m, base, rix, ymax, worst);
+      boot_lane<4>(x << 16, n, nlo8, nhi, M, nr, m, muni, base, rix, ymax, worst);
     else if (mmax == 5)
-      boot_lane<5>(x << 16, n, nlo8, nhi, M, nr, m, base, rix, ymax, worst);
+      boot_lane<5>(x << 16, n, nlo8, nhi, M, nr, m, muni, base, rix, ymax, worst);
     else
-      boot_lane<8>(x << 16, n, nlo8, nhi, M, nr, m, base, rix, ymax, worst);
+      boot_lane<8>(x << 16, n, nlo8, nhi, M, nr, m, muni, base, rix, ymax, worst);
     if (worst < base) atomicOr(&sh_bad[wl], FW_BAD_GENERAL);
     if ((ymax >> 1) > limit) atomicOr(&sh_bad[wl], FW_BAD_REJECT);
   }
@@ -581,10 +708,14 @@ int gd_fet_window_prepare(int64_t wtotal, int32_t *slow_list, unsigned *slow_cou
 }
 
 /* workgroups [blk_begin, blk_begin + blk_count) of the chromosome-aligned grid */
+/* fused: the span scores come from avals/bvals and the score table (snp_score is then
+ * read only for chromosomes whose sizes the table does not hold) */
 int gd_fet_window_fast_launch(const gd_chrom_dev *ch, int nchrom, const int32_t *blk_off, int blk_begin,
                               int blk_count, const int32_t *lo_a, const int32_t *hi_a, const int32_t *lo_b,
-                              const double *snp_score, double perc, double *scores, double *stddev,
-                              unsigned *flags, int32_t *slow_list, unsigned *slow_count, hipStream_t s) {
+                              const double *snp_score, const double *avals, const double *bvals,
+                              const uint64_t *binom, const int *lut_hdr, const double *lut, int fused, double perc,
+                              double *scores, double *stddev, unsigned *flags, int32_t *slow_list,
+                              unsigned *slow_count, hipStream_t s) {
   if (blk_count <= 0) return GD_OK;
 #ifdef GD_FET_PROFILE
   {
@@ -597,6 +728,7 @@ int gd_fet_window_fast_launch(const gd_chrom_dev *ch, int nchrom, const int32_t 
   }
 #endif
   hipLaunchKernelGGL(k_fet_window_fast, dim3((unsigned)blk_count), dim3(FW_WPB * FW_TPW), 0, s, ch, nchrom, blk_off,
-                     blk_begin, lo_a, hi_a, lo_b, snp_score, perc, scores, stddev, flags, slow_list, slow_count);
+                     blk_begin, lo_a, hi_a, lo_b, snp_score, avals, bvals, binom, lut_hdr, lut, fused, perc, scores,
+                     stddev, flags, slow_list, slow_count);
   return hipGetLastError() == hipSuccess ? GD_OK : GD_ERR_HIP;
 }

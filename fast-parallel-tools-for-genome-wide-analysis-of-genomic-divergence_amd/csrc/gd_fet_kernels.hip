@@ -15,83 +15,13 @@
  * All FP arithmetic is compiled with -ffp-contract=off (the reference build has no FMA).
  */
 #include "gd_common.h"
+#include "gd_fet_rows.h"
 #include "gd_internal.h"
 
 namespace {
 
 __device__ __forceinline__ int64_t fdiv(int64_t a, int64_t b) { return a >= 0 ? a / b : -((-a + b - 1) / b); }
 __device__ __forceinline__ int64_t cdiv(int64_t a, int64_t b) { return -fdiv(-a, b); }
-
-__device__ __forceinline__ uint64_t binom_at(const uint64_t *tab, int n, int k) {
-  if (n >= 0 && k >= 0 && k <= n && n <= GD_BINOM_NMAX) return tab[gd_binom_index(n, k)];
-  return gd_binomial_ref((uint64_t)(int64_t)n, (uint64_t)(int64_t)k);
-}
-
-/* binomial lookups go through a kernel-local table pointer */
-struct BinomTab {
-  const uint64_t *t;
-  __device__ __forceinline__ uint64_t operator()(int n, int k) const { return binom_at(t, n, k); }
-};
-
-/* the table buffer's mode word (reference / exact, gd_common.h) */
-__device__ __forceinline__ int fet_mode(const uint64_t *tab) { return (int)tab[GD_FET_MODE_WORD]; }
-
-__device__ double fet_p_two_tailed(int a, int b, int c, int d, const uint64_t *tab) {
-  BinomTab B{tab};
-  const bool exact = fet_mode(tab) != 0;
-  const double *lfh = reinterpret_cast<const double *>(tab + GD_FET_LF_OFF), *lfl = lfh + (GD_BINOM_NMAX + 1);
-  auto table_p = [&](const int *g) {
-    return exact ? gd_fet_table_p_exact(lfh, lfl, g[0], g[1], g[2], g[3]) : GD_FET_TABLE_P(B, g[0], g[1], g[2], g[3]);
-  };
-  const int tie = (a + b == c + d) || (a + c == b + d);
-  int f[4] = {a, b, c, d};
-  gd_table_min_to_a(f);
-  const double p0 = table_p(f);
-  double tot = p0, step = p0;
-  while (f[0] > 0) {
-    f[1]++;
-    f[2]++;
-    step = (1.0 * f[0] * f[3]) / (double)(f[1] * f[2]) * step;
-    tot += step;
-    f[0]--;
-    f[3]--;
-  }
-  if (tie) {
-    tot = 2 * tot;
-  } else {
-    gd_table_opposite_extreme(f);
-    gd_table_min_to_a(f);
-    double far = table_p(f);
-    while (far < (exact ? p0 * (1.0 - GD_FET_EXACT_TIE) : p0)) {
-      tot += far;
-      if (f[1] == 0 || f[2] == 0) break;
-      f[0]++;
-      f[3]++;
-      far = (1.0 * f[1] * f[2]) / (double)(f[0] * f[3]) * far;
-      f[1]--;
-      f[2]--;
-    }
-  }
-  if (tot > 1) tot = 1;
-  return tot;
-}
-
-/* fetcount(): exact double compares against 3 and -3 (cFisher.c:208-238) */
-__device__ __forceinline__ double snp_score_raw(const double *a, int asize, const double *b, int bsize,
-                                                const uint64_t *tab) {
-  int f0 = 0, f1 = 0, f2 = 0, f3 = 0;
-  for (int k = 0; k < asize; ++k) {
-    const double v = a[k];
-    f0 += (v == 3.0);
-    f1 += (v == -3.0);
-  }
-  for (int k = 0; k < bsize; ++k) {
-    const double v = b[k];
-    f2 += (v == 3.0);
-    f3 += (v == -3.0);
-  }
-  return gd_fet_score_from_p(fet_p_two_tailed(f0, f1, f2, f3, tab));
-}
 
 __device__ __forceinline__ int chrom_of(const gd_chrom_dev *ch, int nchrom, int64_t g) {
   int lo = 0, hi = nchrom - 1;
@@ -255,38 +185,17 @@ __global__ void __launch_bounds__(256) k_bounds(const gd_chrom_dev *ch, const in
 /* -log10.  Values are read once from HBM at full width; the FP compare is the     */
 /* reference's exact double compare (fetcount, cFisher.c:216-233).               */
 /* ------------------------------------------------------------------------ */
-#define SF_MAXCH 168 /* 128-element chunks per population per tile */
-
-namespace {
-
-__device__ __forceinline__ uint64_t lane_range(int a, int b) {
-  const uint64_t hi = (b >= 64) ? ~0ull : ((1ull << b) - 1);
-  const uint64_t lo = (a >= 64) ? ~0ull : ((1ull << a) - 1);
-  return hi & ~lo;
-}
-
-/* bits set among tile-relative elements [s, e) of one (pop, kind) mask set */
-__device__ __forceinline__ int count_range(const uint64_t (*m)[2], int s, int e) {
-  int cnt = 0;
-  for (int k = s >> 7; k <= (e - 1) >> 7; ++k) {
-    const int ls = max(s - (k << 7), 0), le = min(e - (k << 7), 128);
-    cnt += __popcll(m[k][0] & lane_range((ls + 1) >> 1, (le + 1) >> 1)) +
-           __popcll(m[k][1] & lane_range(ls >> 1, le >> 1));
-  }
-  return cnt;
-}
-
-}  // namespace
-
+/* skip_table_held: fused scans score rows inside the window kernel whenever the
+ * score table holds the chromosome's sizes; only the other chromosomes run here */
 __global__ void __launch_bounds__(256) k_snp_fet(const gd_chrom_dev *ch, const double *avals, const double *bvals,
                                                  const uint64_t *binom, const int *lut_hdr, const double *lut,
-                                                 double *snp_score) {
+                                                 double *snp_score, int skip_table_held) {
   __shared__ uint64_t sh_m[2][2][SF_MAXCH][2]; /* [pop][maj/min][chunk][even/odd] */
   const gd_chrom_dev &d = ch[blockIdx.y];
   if (d.wend <= 0) return;
   const int nrows = d.nrows, asize = d.asize, bsize = d.bsize;
-  const bool use_lut =
-      lut_hdr[2] == 1 && lut_hdr[0] == asize && lut_hdr[1] == bsize && lut_hdr[3] == fet_mode(binom);
+  const bool use_lut = gd_lut_holds(lut_hdr, asize, bsize, binom);
+  if (use_lut && skip_table_held) return;
   const int lut_nb = (bsize + 1) * (bsize + 2) / 2;
   const int big = max(asize, bsize);
   const int R = min(256, ((SF_MAXCH - 2) * 128) / max(big, 1));
@@ -484,8 +393,9 @@ __global__ void __launch_bounds__(BLOCK)
     k_fet_window_general(const gd_chrom_dev *ch, int nchrom, const int32_t *wlist, const unsigned *wlist_count,
                          int64_t wtotal, const int32_t *lo_a, const int32_t *hi_a, const int32_t *lo_b,
                          const double *avals, const double *bvals, const double *snp_score,
-                         const uint64_t *binom, double perc, double *scores, double *stddev, unsigned *flags,
-                         int32_t *huge_list, unsigned *huge_count, double *gscratch, int64_t gscratch_n) {
+                         const uint64_t *binom, const int *lut_hdr, const double *lut, double perc, double *scores,
+                         double *stddev, unsigned *flags, int32_t *huge_list, unsigned *huge_count,
+                         double *gscratch, int64_t gscratch_n) {
   __shared__ double sh_rep[GD_NREP];
   __shared__ int sh_scan[BLOCK];
   __shared__ uint64_t sh_x;
@@ -545,9 +455,13 @@ __global__ void __launch_bounds__(BLOCK)
     if (tid == 0) sh_nan = 0;
     __syncthreads();
     int has_nan = 0;
+    const bool held = lut_hdr && gd_lut_holds(lut_hdr, asize, bsize, binom);
     for (int i = tid; i < n; i += BLOCK) {
       double v;
-      if (aligned)
+      if (held) /* fused scans keep per-SNP scores only where the table misses */
+        v = snp_score_table(avals + d.a_off + lo + (int64_t)i * asize, asize,
+                            bvals + d.b_off + lb + (int64_t)i * bsize, bsize, lut);
+      else if (aligned)
         v = snp_score[d.a_off + lo / asize + i];
       else
         v = snp_score_raw(avals + d.a_off + lo + (int64_t)i * asize, asize,
@@ -647,11 +561,11 @@ template __global__ void k_fet_window_general<64, false>(const gd_chrom_dev *, i
                                                          const unsigned *, int64_t, const int32_t *,
                                                          const int32_t *, const int32_t *, const double *,
                                                          const double *, const double *, const uint64_t *,
-                                                         double, double *, double *, unsigned *, int32_t *,
-                                                         unsigned *, double *, int64_t);
+                                                         const int *, const double *, double, double *, double *,
+                                                         unsigned *, int32_t *, unsigned *, double *, int64_t);
 template __global__ void k_fet_window_general<256, true>(const gd_chrom_dev *, int, const int32_t *,
                                                          const unsigned *, int64_t, const int32_t *,
                                                          const int32_t *, const int32_t *, const double *,
                                                          const double *, const double *, const uint64_t *,
-                                                         double, double *, double *, unsigned *, int32_t *,
-                                                         unsigned *, double *, int64_t);
+                                                         const int *, const double *, double, double *, double *,
+                                                         unsigned *, int32_t *, unsigned *, double *, int64_t);
