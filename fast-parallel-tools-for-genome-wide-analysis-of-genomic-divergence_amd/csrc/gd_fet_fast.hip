@@ -271,66 +271,71 @@ __device__ __forceinline__ double group8_max(double v) {
   return v;
 }
 
-/* Per-SNP scores of chromosome rows [r0, r0 + nrows) into dst[0 .. nrows): tiles of
- * R rows; the workgroup's waves stream each tile's A and B values (four 16-byte
- * loads per lane in flight), ballot them into "== 3" / "== -3" masks in LDS, then
- * one thread per row counts its popcounts and looks the score table up (the caller
- * checked that the table holds this chromosome's sizes). */
+/* Per-SNP scores of chromosome rows [r0, r0 + nrows) (nrows <= FW_SPAN) into
+ * dst[0 .. nrows): fetcount (cFisher.c:208-238) as LDS atomics into one word per
+ * row holding four byte counters (majA, minA, majB, minB; population sizes < 256),
+ * then the score-table lookup (the caller checked that the table holds these sizes).
+ * The workgroup's waves stream the rows' A and B values with four 16-byte loads per
+ * lane in flight; a value's row is one v_mul_hi_u32 by ceil(2^32 / size), exact for
+ * the < 2^18 element offsets of a span. */
 __device__ void fw_stage_scores(const gd_chrom_dev &d, int r0, int nrows, const double *avals, const double *bvals,
-                                const double *lut, uint64_t (*m)[2][SF_MAXCH][2], double *dst) {
+                                const double *lut, uint32_t *cnt, double *dst) {
   constexpr int NT = FW_WPB * FW_TPW, NW = NT / 64;
   const int asize = d.asize, bsize = d.bsize;
   const int lut_nb = (bsize + 1) * (bsize + 2) / 2;
-  const int R = min(NT, ((SF_MAXCH - 2) * 128) / max(max(asize, bsize), 1));
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  for (int t0 = 0; t0 < nrows; t0 += R) {
-    const int rows = min(R, nrows - t0);
-    int rel0[2];
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (nrows <= 0) return; /* workgroup-uniform: no fast window, no span */
+  for (int r = threadIdx.x; r < nrows; r += NT) cnt[r] = 0;
+  __syncthreads();
 #pragma unroll
-    for (int pop = 0; pop < 2; ++pop) {
-      const int size = pop ? bsize : asize;
-      const double *vals = pop ? bvals : avals;
-      const int64_t start = (pop ? d.b_off : d.a_off) + (int64_t)(r0 + t0) * size;
-      const int64_t stop = start + (int64_t)rows * size;
-      const int64_t gb = start & ~(int64_t)1; /* 16-byte aligned element */
-      rel0[pop] = (int)(start - gb);
-      const int nch = (int)((stop - gb + 127) >> 7);
-      for (int k0 = wave; k0 < nch; k0 += 4 * NW) {
-        double2 v[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int64_t e = gb + ((int64_t)(k0 + u * NW) << 7) + 2 * lane;
-          v[u].x = 0.0;
-          v[u].y = 0.0;
-          if (e + 1 < stop)
-            v[u] = *reinterpret_cast<const double2 *>(vals + e);
-          else if (e < stop)
-            v[u].x = vals[e];
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int k = k0 + u * NW;
-          const uint64_t ja = __ballot(v[u].x == 3.0), jb = __ballot(v[u].y == 3.0);
-          const uint64_t na = __ballot(v[u].x == -3.0), nb = __ballot(v[u].y == -3.0);
-          if (lane == 0 && k < nch) {
-            m[pop][0][k][0] = ja;
-            m[pop][0][k][1] = jb;
-            m[pop][1][k][0] = na;
-            m[pop][1][k][1] = nb;
-          }
-        }
+  for (int pop = 0; pop < 2; ++pop) {
+    const int size = pop ? bsize : asize;
+    const uint32_t rmul = (uint32_t)((0xFFFFFFFFull + size) / size); /* ceil(2^32 / size) */
+    const uint32_t inc3 = 1u << (16 * pop), incm3 = 1u << (16 * pop + 8);
+    const double *vals = pop ? bvals : avals;
+    const int64_t start = (pop ? d.b_off : d.a_off) + (int64_t)r0 * size;
+    const int64_t stop = start + (int64_t)nrows * size;
+    const int64_t gb = start & ~(int64_t)1; /* 16-byte aligned element */
+    const int rel0 = (int)(gb - start);     /* 0 or -1 */
+    const int nel = (int)(stop - start);
+    const int nch = (int)((stop - gb + 127) >> 7);
+    const int nfull = (int)((stop - gb) >> 7); /* chunks wholly inside [gb, stop) */
+    const double2 *v2 = reinterpret_cast<const double2 *>(vals + gb);
+    /* full chunks: only x of chunk 0, lane 0 can fall outside (element start - 1 of
+     * an odd start); the partial last chunk also masks elements past the span */
+    auto count_pair = [&](double x, double y, int k, bool partial) {
+      const int rel = rel0 + (k << 7) + 2 * lane; /* element offset of x from start */
+      uint32_t ix = x == 3.0 ? inc3 : (x == -3.0 ? incm3 : 0u);
+      uint32_t iy = y == 3.0 ? inc3 : (y == -3.0 ? incm3 : 0u);
+      int relx = max(rel, 0), rely = rel + 1;
+      if (rel < 0) ix = 0;
+      if (partial) {
+        if (rel + 1 >= nel) iy = 0;
+        if (rel >= nel) ix = 0;
+        relx = min(relx, nel - 1);
+        rely = min(rely, nel - 1);
       }
+      atomicAdd(&cnt[__umulhi((uint32_t)relx, rmul)], ix);
+      atomicAdd(&cnt[__umulhi((uint32_t)rely, rmul)], iy);
+    };
+    for (int k0 = wave; k0 < nfull; k0 += 4 * NW) {
+      double2 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = v2[min(k0 + u * NW, nfull - 1) * 64 + lane];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (k0 + u * NW < nfull) count_pair(v[u].x, v[u].y, k0 + u * NW, false);
     }
-    __syncthreads();
-    for (int r = threadIdx.x; r < rows; r += NT) {
-      const int sa = rel0[0] + r * asize, sb = rel0[1] + r * bsize;
-      const int f0 = count_range(m[0][0], sa, sa + asize);
-      const int f1 = count_range(m[0][1], sa, sa + asize);
-      const int f2 = count_range(m[1][0], sb, sb + bsize);
-      const int f3 = count_range(m[1][1], sb, sb + bsize);
-      dst[t0 + r] = lut[(int64_t)gd_pair_index(f0, f1, asize) * lut_nb + gd_pair_index(f2, f3, bsize)];
+    if (nfull < nch && wave == NW - 1) { /* the partial last chunk, element by element */
+      const int64_t e = gb + ((int64_t)nfull << 7) + 2 * lane;
+      count_pair(e < stop ? vals[e] : 0.0, e + 1 < stop ? vals[e + 1] : 0.0, nfull, true);
     }
-    __syncthreads();
+  }
+  __syncthreads();
+  for (int r = threadIdx.x; r < nrows; r += NT) {
+    const uint32_t c = cnt[r];
+    const int f0 = c & 255, f1 = (c >> 8) & 255, f2 = (c >> 16) & 255, f3 = c >> 24;
+    dst[r] = lut[(int64_t)gd_pair_index(f0, f1, asize) * lut_nb + gd_pair_index(f2, f3, bsize)];
   }
 }
 
@@ -366,14 +371,14 @@ __global__ void __launch_bounds__(FW_WPB *FW_TPW)
                       const double *lut, int fused, double perc, double *scores, double *stddev,
                       const unsigned *flags, int32_t *slow_list, unsigned *slow_count) {
   __shared__ double sh_span[FW_SPAN];
-  /* the ballot masks of the span staging (fused mode) share LDS with the ranked top
+  /* the row counters of the span staging (fused mode) share LDS with the ranked top
    * scores and the replicate rank pairs, which are written only after it */
   __shared__ union {
     struct {
       double top[FW_WPB][FW_KTOP];
       uint16_t rix[FW_WPB][FW_TPW * FW_RPT]; /* per replicate: rank pair read (rix_pack) */
     } b;
-    uint64_t m[2][2][SF_MAXCH][2]; /* [pop][== 3 / == -3][chunk][even / odd element] */
+    uint32_t cnt[FW_SPAN]; /* per span row: majA | minA << 8 | majB << 16 | minB << 24 */
   } sh_u;
   double(&sh_top)[FW_WPB][FW_KTOP] = sh_u.b.top;
   uint16_t(&sh_rix)[FW_WPB][FW_TPW * FW_RPT] = sh_u.b.rix;
@@ -452,10 +457,15 @@ __global__ void __launch_bounds__(FW_WPB *FW_TPW)
   }
   const int64_t span0 = (int64_t)sh_lo;
   const int spanlen = sh_hi > sh_lo ? (int)(sh_hi - sh_lo) : 0;
-  if (fused && gd_lut_holds(lut_hdr, d.asize, d.bsize, binom)) {
+#ifdef GD_FET_NOSTAGE
+  if (true) { /* diagnostics: span without scores (cost of everything else) */
+    for (int i = tid; i < spanlen; i += FW_WPB * FW_TPW) sh_span[i] = (double)(i % 7);
+  } else
+#endif
+  if (spanlen > 0 && fused && gd_lut_holds(lut_hdr, d.asize, d.bsize, binom)) {
     /* fused: the span rows' -log10 p from the genotype values (fetcount + the score
      * table, as k_snp_fet) -- the values are read here, once per workgroup */
-    fw_stage_scores(d, (int)(span0 - d.a_off), spanlen, avals, bvals, lut, sh_u.m, sh_span);
+    fw_stage_scores(d, (int)(span0 - d.a_off), spanlen, avals, bvals, lut, sh_u.cnt, sh_span);
   } else {
     /* k_snp_fet scored the rows (unfused mode, or sizes the table does not hold) */
     for (int i = tid; i < spanlen; i += FW_WPB * FW_TPW) sh_span[i] = snp_score[span0 + i];
