@@ -659,16 +659,20 @@ __global__ void __launch_bounds__(FW_WPB *FW_TPW)
     if (step > 0) sum = dpp_f64<0x101>(sum); /* row_shl:1: lane l takes lane l+1's partial */
   }
   const double mu = __shfl(sum, (int)(threadIdx.x & ~7u)) / GD_NREP;
+  /* the squared deviations off the chain, all lanes at once (no FMA: the same two
+   * roundings as the reference's (x - m) * (x - m)); the chain only adds */
+#pragma unroll
+  for (int k = 0; k < FW_RPT; ++k) {
+    const double dd = rep[k] - mu;
+    rep[k] = dd * dd;
+  }
   double ss = 0.0;
 #pragma unroll
   for (int step = FW_TPW - 1; step >= 0; --step) {
     if (live && q == step) {
 #pragma unroll
       for (int k = FW_RPT - 1; k >= 0; --k)
-        if (k < nr) {
-          const double dd = rep[k] - mu;
-          ss += dd * dd;
-        }
+        if (k < nr) ss += rep[k];
     }
     if (step > 0) ss = dpp_f64<0x101>(ss);
   }

@@ -109,16 +109,16 @@ __global__ void __launch_bounds__(256) k_bounds(const gd_chrom_dev *ch, const in
   int32_t *hi = hi_a + d.w_base;
   const double inv = 1.0 / (double)wstep;
   const bool aligned16 = ((pop ? d.b_off : d.a_off) & 3) == 0; /* int4 loads stay 16-byte aligned */
-  /* each lane scans 16 consecutive elements (chromosome-relative i in [i0, i0+16)),
-   * packs the offsets of its boundaries (i == 0, i == len, or pos[i] != pos[i-1])
-   * as 4-bit nibbles, then handles just those: a wave runs the window-range code
-   * max-boundaries-per-lane times (~1-2 at 20 individuals), not once per element */
+  /* each lane scans 16 consecutive elements (chromosome-relative i in [i0, i0+16)):
+   * bit k of `bits` marks a boundary (i == 0, i == len, or pos[i] != pos[i-1]; three
+   * VALU per element: unsigned difference, min with 1, shift-or), then the lane walks
+   * just those bits: a wave runs the window-range code max-boundaries-per-lane times
+   * (~1-2 at 20 individuals), not once per element */
   const int64_t stride = (int64_t)gridDim.x * blockDim.x * 16;
   bool unsorted = false;
   for (int64_t i0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 16; i0 <= len; i0 += stride) {
     int32_t prev = (i0 > 0) ? pos[i0 - 1] : 0;
-    uint64_t nib = 0;
-    int nb = 0;
+    uint32_t bits = 0;
     if (i0 + 16 <= len) {
       int32_t v16[16];
       if (aligned16) {
@@ -134,28 +134,34 @@ __global__ void __launch_bounds__(256) k_bounds(const gd_chrom_dev *ch, const in
 #pragma unroll
         for (int k = 0; k < 16; ++k) v16[k] = pos[i0 + k];
       }
+      bool dec = false;
 #pragma unroll
       for (int k = 0; k < 16; ++k) {
         const int32_t v = v16[k];
-        const bool bnd = (v != prev) || (i0 + k == 0);
-        unsorted |= (i0 + k > 0) && (v < prev);
-        nib |= bnd ? ((uint64_t)k << (4 * nb)) : 0;
-        nb += bnd;
+        bits |= min((uint32_t)v - (uint32_t)prev, 1u) << k;
+        dec |= v < prev;
         prev = v;
       }
+      if (i0 == 0) {
+        bits |= 1u; /* element 0 opens the first run; it has no predecessor */
+        dec = false;
+#pragma unroll
+        for (int k = 1; k < 16; ++k) dec |= v16[k] < v16[k - 1];
+      }
+      unsorted |= dec;
     } else {
       for (int k = 0; k < 16 && i0 + k <= len; ++k) {
         const int64_t i = i0 + k;
         const int32_t v = (i < len) ? pos[i] : 0;
         const bool bnd = (i == 0) || (i == len) || (v != prev);
         if (i > 0 && i < len) unsorted |= (v < prev);
-        nib |= bnd ? ((uint64_t)k << (4 * nb)) : 0;
-        nb += bnd;
+        bits |= bnd ? 1u << k : 0u;
         prev = v;
       }
     }
-    for (int t = 0; t < nb; ++t) {
-      const int64_t i = i0 + (int)((nib >> (4 * t)) & 15);
+    while (bits) {
+      const int64_t i = i0 + __builtin_ctz(bits);
+      bits &= bits - 1;
       const bool first = (i == 0), last = (i == len);
       const int64_t p = last ? 0 : pos[i];
       const int64_t pp = first ? 0 : pos[i - 1];
