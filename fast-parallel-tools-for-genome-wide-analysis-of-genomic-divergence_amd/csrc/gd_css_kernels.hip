@@ -59,6 +59,9 @@ __device__ unsigned long long g_css_prof[8];
 #ifndef CSS_STATIC_G2_MAX
 #define CSS_STATIC_G2_MAX 80 /* largest G = 2 tier with compile-time-K steps */
 #endif
+#ifndef CSS_BISECT_TOL
+#define CSS_BISECT_TOL 1e-9 /* bisection stops at this fraction of the spectral bound */
+#endif
 #ifndef CSS_MDS_WAVES
 #define CSS_MDS_WAVES(MP) ((MP) <= 24 ? 5 : (MP) <= 40 ? 4 : (MP) <= 64 ? 2 : (MP) <= 96 ? 3 : 2)
 #endif
@@ -883,6 +886,7 @@ __global__ void __launch_bounds__((CssShape<MP, G>::NT), CSS_MDS_WAVES(MP))
       if (tid >= m && tid < MP + 4) s_d[tid] = 2.0 * fabs(ghi) + 2.0 * fabs(glo) + 1.0;
     }
     const int m4 = (m + 3) & ~3;
+    const double bis_tol = CSS_BISECT_TOL * fmax(fabs(glo), fabs(ghi)) + DBL_MIN;
     __syncthreads();
     if (tid < 64) {
       const int hh = tid >> 5, j = tid & 31;
@@ -925,13 +929,13 @@ __global__ void __launch_bounds__((CssShape<MP, G>::NT), CSS_MDS_WAVES(MP))
         const bool same = (nl == l && nu == u);
         l = nl;
         u = nu;
-        const bool conv = same || (u - l) <= 2.0 * DBL_EPSILON * fmax(fabs(l), fabs(u)) + DBL_MIN;
+        /* a shift within CSS_BISECT_TOL ||T|| is all inverse iteration needs (its two
+         * solves gain (shift error / gap)^2 on the eigenvector); the eigenvalue itself
+         * comes back to rounding as the Rayleigh quotient below */
+        const bool conv = same || (u - l) <= bis_tol;
         if (__all(conv)) break;
       }
-      if (j == 0) {
-        const double lam = 0.5 * (l + u);
-        s_lam[hh] = fabs(lam) <= zero_tol ? 0.0 : lam;
-      }
+      if (j == 0) s_lam[hh] = 0.5 * (l + u);
     }
     __syncthreads();
 
@@ -1025,6 +1029,29 @@ __global__ void __launch_bounds__((CssShape<MP, G>::NT), CSS_MDS_WAVES(MP))
       zero = 0.0;
       block_sum2<NW>(n2, zero, s_red);
       y2 *= 1.0 / sqrt(n2);
+    }
+    /* eigenvalues = Rayleigh quotients y^T T y of the unit vectors (error ~ the
+     * squared eigenvector error, far below rounding) */
+    {
+      __syncthreads();
+      if (lead && row) {
+        s_y[0][i] = y1;
+        s_y[1][i] = y2;
+      }
+      __syncthreads();
+      double t1 = 0.0, t2 = 0.0;
+      if (lead && row) {
+        const double el = i > 0 ? s_e[i - 1] : 0.0, er = i + 1 < m ? s_e[i] : 0.0;
+        const int il = i > 0 ? i - 1 : 0, ir = i + 1 < m ? i + 1 : i;
+        t1 = y1 * (s_d[i] * y1 + el * s_y[0][il] + er * s_y[0][ir]);
+        t2 = y2 * (s_d[i] * y2 + el * s_y[1][il] + er * s_y[1][ir]);
+      }
+      block_sum2<NW>(t1, t2, s_red);
+      if (tid == 0) {
+        s_lam[0] = fabs(t1) <= zero_tol ? 0.0 : t1;
+        s_lam[1] = fabs(t2) <= zero_tol ? 0.0 : t2;
+      }
+      __syncthreads();
     }
 
     CSS_PROF(4);
