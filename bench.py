@@ -12,8 +12,11 @@ Prints ONE JSON line (rank 0).  `roofline` prices the whole scan's algorithmic
 HBM bytes B = 12*(alen+blen) + 16*W (f64 value + i32 position per
 genotype, two f64 outputs per window) against its kernel time, and also lists each
 stage's kernel time.  `traffic` is the measured HBM bytes per scan from the committed
-rocprofv3 PMC summary (profiles/r01_fet_traffic.json, FETCH_SIZE doubled per the
-gfx950 correction + WRITE_SIZE), or null when absent.  `cpu_baseline` times the
+rocprofv3 PMC summary (profiles/r02_fet_traffic.json, FETCH_SIZE doubled per the
+gfx950 correction + WRITE_SIZE), or null when absent.  The scan is bound by VALU issue
+(the bootstrap's draws), not HBM: `roofline.valu` prices the PMC-counted VALU
+wave-instructions per scan (profiles/r02_fet_valu.json) over this run's scan time
+against the 614 G wave-instructions/s issue peak.  `cpu_baseline` times the
 reference's own Pthreads threadcompute() (oracle/_ref, compiled from the reference
 sources) on a bounded sample of the same workload, or the oracle port when that
 binary is absent.
@@ -42,7 +45,12 @@ sys.path.insert(0, str(PKG))
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, HBM3E spec
 FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 vector spec; ubench: ~31-37 T FMA/s
-TRAFFIC_FILE = ROOT / "profiles" / "r01_fet_traffic.json"
+PROFILE_ROUND = "r02"
+TRAFFIC_FILE = ROOT / "profiles" / f"{PROFILE_ROUND}_fet_traffic.json"
+VALU_FILE = ROOT / "profiles" / f"{PROFILE_ROUND}_fet_valu.json"
+# VALU issue peak: 256 CUs x 4 SIMDs, one wave64 VALU instruction per 4 cycles per SIMD
+# at the 2.4 GHz max clock (MI355X_MICROARCH.md) = 614.4 G wave-instructions/s
+VALU_PEAK_GINSTS = 256 * 4 * 2.4 / 4
 
 
 def parse():
@@ -401,6 +409,17 @@ def main():
         if tr.get("config") == [nch, nsnp, a, b]:
             out["roofline"]["traffic"] = tr["bytes_per_scan"]
             out["roofline"]["traffic_source"] = f"{TRAFFIC_FILE.relative_to(ROOT)} ({tr['method']})"
+    if VALU_FILE.exists():
+        # the binding resource of the scan: VALU issue (the bootstrap's nrand48 draws),
+        # not HBM -- wave-instructions per scan (PMC SQ_INSTS_VALU, committed profile)
+        # over this run's scan time, against the VALU issue peak
+        vr = json.loads(VALU_FILE.read_text())
+        if vr.get("config") == [nch, nsnp, a, b]:
+            ginst = vr["valu_wave_insts_per_scan"] / (stage[3] * 1e-3) / 1e9
+            out["roofline"]["valu"] = {
+                "bound": "valu-issue", "achieved": ginst, "peak": VALU_PEAK_GINSTS, "unit": "G wave-insts/s",
+                "frac": ginst / VALU_PEAK_GINSTS, "insts_per_scan": vr["valu_wave_insts_per_scan"],
+                "source": f"{VALU_FILE.relative_to(ROOT)} ({vr['method']})"}
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(args)
 

@@ -2,9 +2,9 @@
 # One GPU-box profiling pass for a round: bench line, kernel trace + stats, and the
 # HBM PMC counters (FETCH_SIZE and WRITE_SIZE in separate passes).  Every GPU step
 # has its own time limit and the steps are chained with &&.
-# usage: tools/profile_round.sh r01
+# usage: tools/profile_round.sh r02
 set -o pipefail
-R=${1:-r01}
+R=${1:-r02}
 O=gpurun_out/$R
 mkdir -p $O
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
@@ -15,6 +15,8 @@ timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $O/pmc_fetch -o run --output-for
     python3 bench.py --steps 2 --warmup 1 --no-cpu --no-css > $O/pmc_fetch.json 2> $O/pmc_fetch.err &&
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d $O/pmc_write -o run --output-format csv -- \
     python3 bench.py --steps 2 --warmup 1 --no-cpu --no-css > $O/pmc_write.json 2> $O/pmc_write.err &&
+timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES SQ_INSTS_SALU SQ_INSTS_LDS -d $O/pmc_valu -o run --output-format csv -- \
+    python3 bench.py --steps 2 --warmup 1 --no-cpu --no-css > $O/pmc_valu.json 2> $O/pmc_valu.err &&
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $O/pmc_css_fetch -o run --output-format csv -- \
     python3 bench.py --steps 1 --warmup 0 --no-cpu --css-steps 1 > $O/pmc_css.json 2> $O/pmc_css.err
 echo "profile_round exit $?"

@@ -2,6 +2,7 @@
   profiles/<R>_kernel_stats.csv   rocprofv3 --stats summary of the bench command
   profiles/<R>_bench.json         the bench line measured in the same call
   profiles/<R>_fet_traffic.json   HBM bytes per FET scan from the PMC passes
+  profiles/<R>_fet_valu.json      VALU wave-instructions per FET scan (SQ_INSTS_VALU)
   profiles/<R>_summary.md         per-kernel averages, per-scan traffic, cross-checks
 """
 import csv
@@ -12,7 +13,7 @@ from collections import defaultdict
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parent.parent
-R = sys.argv[1] if len(sys.argv) > 1 else "r01"
+R = sys.argv[1] if len(sys.argv) > 1 else "r02"
 src = ROOT / "gpurun_out" / R
 dst = ROOT / "profiles"
 dst.mkdir(exist_ok=True)
@@ -71,6 +72,18 @@ traffic = {
 }
 (dst / f"{R}_fet_traffic.json").write_text(json.dumps(traffic, indent=1) + "\n")
 
+valu, nv = counters(src / "pmc_valu", "SQ_INSTS_VALU")
+vscans = nv.get("k_popsize", 0)
+vk = {k: v for k, v in valu.items() if k.startswith(FET_KERNELS)}
+valu_doc = {
+    "config": traffic["config"],
+    "valu_wave_insts_per_scan": sum(vk.values()) / vscans,
+    "scans": vscans,
+    "method": "rocprofv3 --pmc SQ_INSTS_VALU over the FET scan kernels (wave-instructions)",
+    "per_kernel_per_scan": {k: v / vscans for k, v in sorted(vk.items())},
+}
+(dst / f"{R}_fet_valu.json").write_text(json.dumps(valu_doc, indent=1) + "\n")
+
 rows = list(csv.DictReader(open(stats)))
 lines = [f"# {R} profile summary", "", "Command: `rocprofv3 --kernel-trace --stats -- python3 bench.py --steps 5 "
          "--warmup 1 --no-cpu` (FET + CSS legs), PMC passes separate (tools/profile_round.sh).", "",
@@ -81,6 +94,9 @@ for r in rows:
 alg = bench["roofline"]["alg_bytes_per_step"]
 lines += ["", f"FET scan HBM traffic (PMC): {traffic['bytes_per_scan'] / 1e9:.3f} GB per scan "
           f"(fetch {fetch_b / 1e9:.3f} + write {write_b / 1e9:.3f}); algorithmic B = {alg / 1e9:.3f} GB.",
+          "", f"FET scan VALU (PMC SQ_INSTS_VALU): {valu_doc['valu_wave_insts_per_scan'] / 1e9:.3f} G wave-instructions "
+          f"per scan; at the bench's scan time that is {valu_doc['valu_wave_insts_per_scan'] / (bench['roofline']['stage_ms']['scan_total'] * 1e-3) / 1e9:.0f} "
+          "G/s of the 614 G/s issue peak (256 CUs x 4 SIMDs x 2.4 GHz / 4).",
           "", "Bench line (same call):", "", "```", json.dumps(bench), "```"]
 (dst / f"{R}_summary.md").write_text("\n".join(lines) + "\n")
 print("\n".join(lines[:40]))
