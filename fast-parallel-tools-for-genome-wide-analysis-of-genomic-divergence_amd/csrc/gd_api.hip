@@ -43,6 +43,15 @@ __global__ void k_fet_window_general(const gd_chrom_dev *ch, int nchrom, const i
                                      double *stddev, unsigned *flags,
                                      int32_t *huge_list, unsigned *huge_count, double *gscratch,
                                      int64_t gscratch_n);
+int gd_packed_bounds_launch(const gd_chrom_dev *d_ch, int nchrom, const int64_t *row_off, const int32_t *rowpos,
+                            int64_t max_rows, int wsize, int wstep, int32_t *lo_a, int32_t *hi_a, int32_t *lo_b,
+                            unsigned *flags, hipStream_t s);
+int gd_packed_snp_fet_launch(const gd_chrom_dev *d_ch, int nchrom, const int64_t *word_off, const uint64_t *acodes,
+                             const uint64_t *bcodes, int64_t max_rows, const uint64_t *binom, const int *lut_hdr,
+                             const double *lut, double *snp, hipStream_t s);
+int gd_pack_device_launch(const double *avals, const double *bvals, const int32_t *apos, const int32_t *bpos,
+                          int asize, int bsize, int nrows, uint64_t *acodes, uint64_t *bcodes, int32_t *rowpos,
+                          unsigned *bad, hipStream_t s);
 int gd_fet_fast_windows_per_block();
 int gd_fet_fast_init(hipStream_t s);
 int gd_fet_window_prepare(int64_t wtotal, int32_t *slow_list, unsigned *slow_count, hipStream_t s,
@@ -56,9 +65,10 @@ int gd_fet_window_fast_launch(const gd_chrom_dev *ch, int nchrom, const int32_t 
 int gd_css_tier(int m);
 int gd_css_launch(int mp, int drosophila, int mds, const gd_chrom_dev *d_ch, int nchrom, const gd_css_planes *d_pl,
                   uint32_t *planes, const int32_t *lo_a, const int32_t *hi_a, const int32_t *lo_b,
-                  const double *avals, const double *bvals, int64_t wtotal, int64_t max_rows_words, int treshold,
-                  int runs, double *scores, double *p, double *xbuf, uint8_t *status, unsigned *flags,
-                  hipStream_t s, hipEvent_t ev_perm);
+                  const double *avals, const double *bvals, const int64_t *word_off, const uint64_t *acodes,
+                  const uint64_t *bcodes, int64_t wtotal, int64_t max_rows_words, int treshold, int runs,
+                  double *scores, double *p, double *xbuf, uint8_t *status, unsigned *flags, hipStream_t s,
+                  hipEvent_t ev_perm);
 int gd_synth_launch(int chrom, int nsnp, int asize, int bsize, uint64_t seed, const double *freq_table,
                     double *avals, double *bvals, int32_t *apos, int32_t *bpos, hipStream_t s);
 
@@ -102,6 +112,7 @@ struct gd_ctx {
   size_t io_cap = 0;
   hipEvent_t ev[GD_NSTAGES + 1] = {};
   unsigned *h_flags = nullptr; /* pinned */
+  unsigned *h_flags_dev = nullptr; /* one device word (packer status) */
 };
 
 static int ctx_init(gd_ctx *c, int device) {
@@ -144,6 +155,7 @@ static int ctx_init(gd_ctx *c, int device) {
   HIP_TRY(hipMemsetAsync(c->lut_hdr, 0, 4 * sizeof(int), c->stream));
   HIP_TRY(hipMalloc(&c->lut, sizeof(double) * GD_LUT_CAP));
   HIP_TRY(hipHostMalloc(&c->h_flags, 64));
+  HIP_TRY(hipMalloc(&c->h_flags_dev, 64));
   HIP_TRY(hipStreamSynchronize(c->stream));
   return GD_OK;
 }
@@ -175,6 +187,7 @@ extern "C" void gd_ctx_destroy(gd_ctx *c) {
   if (c->stream2) (void)hipStreamDestroy(c->stream2);
   if (c->stream_mem) (void)hipStreamDestroy(c->stream_mem);
   if (c->h_flags) (void)hipHostFree(c->h_flags);
+  if (c->h_flags_dev) (void)hipFree(c->h_flags_dev);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -286,6 +299,55 @@ static int make_plan(const gd_chrom *chroms, int nchrom, int wsize, int wstep, i
   return GD_OK;
 }
 
+/* a packed batch (include/gdscan.h): descriptors and device pointers to the codes */
+struct PackedIn {
+  const gd_pchrom *pc;
+  const uint64_t *acodes, *bcodes;
+  const int32_t *rowpos;
+};
+
+/* the packed chromosomes as their expanded forms: element extents nrows * size, sizes
+ * known up front; a_off = b_off = the first row (the per-SNP score array is indexed
+ * a_off + row, and nothing reads element-indexed values) */
+static int make_plan_packed(const PackedIn &pk, int nchrom, int wsize, int wstep, int window_set, ScanPlan *pl,
+                            std::vector<int64_t> *row_off, std::vector<int64_t> *word_off, int64_t *max_rows) {
+  if (nchrom < 0 || (nchrom > 0 && !pk.pc)) return fail(GD_ERR_ARG, "bad chromosome list");
+  if (nchrom > 0 && (!pk.acodes || !pk.bcodes || !pk.rowpos)) return fail(GD_ERR_ARG, "null packed buffer");
+  std::vector<gd_chrom> ch(nchrom);
+  for (int c = 0; c < nchrom; ++c) {
+    const gd_pchrom &q = pk.pc[c];
+    if (q.nrows < 0 || q.row_off < 0 || q.a_word < 0 || q.b_word < 0) return fail(GD_ERR_ARG, "negative extent");
+    if (q.nrows > 0 && (q.asize <= 0 || q.bsize <= 0)) return fail(GD_ERR_SIZE, "empty population");
+    if ((int64_t)q.nrows * std::max(q.asize, q.bsize) > INT32_MAX) return fail(GD_ERR_SIZE, "chromosome too long");
+    std::memset(&ch[c], 0, sizeof(gd_chrom));
+    ch[c].a_off = ch[c].b_off = q.row_off;
+    ch[c].alen = q.nrows > 0 ? q.nrows * q.asize : 0;
+    ch[c].blen = q.nrows > 0 ? q.nrows * q.bsize : 0;
+    ch[c].regend = q.regend;
+    ch[c].w_out = q.w_out;
+    ch[c].seed = q.seed;
+  }
+  int st = make_plan(ch.data(), nchrom, wsize, wstep, window_set, pl);
+  if (st) return st;
+  row_off->assign(nchrom, 0);
+  word_off->assign(2 * (size_t)nchrom, 0);
+  *max_rows = 1;
+  pl->elems_a = 1;
+  for (int c = 0; c < nchrom; ++c) {
+    const gd_pchrom &q = pk.pc[c];
+    gd_chrom_dev &d = pl->h[c];
+    d.asize = q.asize;
+    d.bsize = q.bsize;
+    d.nrows = q.nrows;
+    (*row_off)[c] = q.row_off;
+    (*word_off)[2 * c] = q.a_word;
+    (*word_off)[2 * c + 1] = q.b_word;
+    *max_rows = std::max<int64_t>(*max_rows, q.nrows);
+    pl->elems_a = std::max<int64_t>(pl->elems_a, q.row_off + q.nrows); /* rows of snp_score */
+  }
+  return GD_OK;
+}
+
 static int flags_to_status(unsigned f) {
   if (f & (GD_FLAG_UNSORTED_A | GD_FLAG_UNSORTED_B)) return fail(GD_ERR_UNSORTED, "positions are not sorted");
   if (f & GD_FLAG_B_BOUNDS) return fail(GD_ERR_BOUNDS, "a window's B slice runs past blen");
@@ -294,15 +356,20 @@ static int flags_to_status(unsigned f) {
 }
 
 /* --------------------------------------------------------------- FET scan */
+/* pk != NULL: a packed batch (chroms, avals .. bpos unused) */
 static int fet_scan_locked(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, const double *avals,
                            const double *bvals, const int32_t *apos, const int32_t *bpos, int wsize, int wstep,
-                           double perc, int mode, int window_set, double *scores, double *stddev, hipStream_t s) {
+                           double perc, int mode, int window_set, double *scores, double *stddev, hipStream_t s,
+                           const PackedIn *pk = nullptr) {
   if (!(perc >= 0.0 && perc <= 1.0)) return fail(GD_ERR_ARG, "percentile must lie in [0, 1]");
   if (mode != GD_FET_REFERENCE && mode != GD_FET_EXACT)
     return fail(GD_ERR_ARG, "FET mode must be GD_FET_REFERENCE (0) or GD_FET_EXACT (1)");
   const uint64_t *binom = mode == GD_FET_EXACT ? ctx->binom_exact : ctx->binom;
   ScanPlan pl;
-  int st = make_plan(chroms, nchrom, wsize, wstep, window_set, &pl);
+  std::vector<int64_t> row_off, word_off;
+  int64_t max_rows = 1;
+  int st = pk ? make_plan_packed(*pk, nchrom, wsize, wstep, window_set, &pl, &row_off, &word_off, &max_rows)
+              : make_plan(chroms, nchrom, wsize, wstep, window_set, &pl);
   if (st) return st;
   for (float &m : g_stage_ms) m = 0.f;
   if (pl.wtotal == 0) return GD_OK;
@@ -330,11 +397,23 @@ static int fet_scan_locked(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, cons
   unsigned *flags;
   int32_t *d_blk, *lo_a, *hi_a, *lo_b, *list, *huge;
   double *snp;
-  layout(cv, &d_ch, &d_blk, &flags, &lo_a, &hi_a, &lo_b, &snp, &list, &huge);
+  int64_t *d_roff = nullptr, *d_woff = nullptr;
+  auto layout_all = [&](Carve &k) {
+    layout(k, &d_ch, &d_blk, &flags, &lo_a, &hi_a, &lo_b, &snp, &list, &huge);
+    if (pk) {
+      d_roff = k.take<int64_t>(nchrom);
+      d_woff = k.take<int64_t>(2 * (size_t)nchrom);
+    }
+  };
+  layout_all(cv);
   if ((st = grow(&ctx->ws, &ctx->ws_cap, cv.off))) return st;
   Carve real{ctx->ws};
-  layout(real, &d_ch, &d_blk, &flags, &lo_a, &hi_a, &lo_b, &snp, &list, &huge);
+  layout_all(real);
   unsigned *list_count = flags + 4, *huge_count = flags + 8;
+  if (pk) {
+    HIP_TRY(hipMemcpyAsync(d_roff, row_off.data(), sizeof(int64_t) * nchrom, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(d_woff, word_off.data(), sizeof(int64_t) * 2 * nchrom, hipMemcpyHostToDevice, s));
+  }
 
   HIP_TRY(hipMemcpyAsync(d_ch, pl.h.data(), sizeof(gd_chrom_dev) * nchrom, hipMemcpyHostToDevice, s));
   HIP_TRY(hipMemcpyAsync(d_blk, blk_off.data(), sizeof(int32_t) * (nchrom + 1), hipMemcpyHostToDevice, s));
@@ -347,7 +426,7 @@ static int fet_scan_locked(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, cons
    * other work. */
   hipStream_t sm = ctx->stream_mem, s2 = ctx->stream2;
   HIP_TRY(hipStreamWaitEvent(sm, ctx->ev[0], 0));
-  hipLaunchKernelGGL(k_popsize, dim3(nchrom), dim3(64), 0, sm, d_ch, apos, bpos, flags);
+  if (!pk) hipLaunchKernelGGL(k_popsize, dim3(nchrom), dim3(64), 0, sm, d_ch, apos, bpos, flags);
   bool force_general = false;
   if ((st = gd_fet_window_prepare(pl.wtotal, list, list_count, sm, &force_general))) return st;
   /* score table for chromosome 0's population sizes (no-op when cached) */
@@ -360,7 +439,7 @@ static int fet_scan_locked(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, cons
    * (k_snp_fet) exits at once, so the only full pass is k_bounds; GD_FET_UNFUSED=1
    * restores the per-SNP pass feeding the window kernel through snp_score */
   const char *uf = getenv("GD_FET_UNFUSED");
-  const bool fused = !(uf && uf[0] == '1');
+  const bool fused = !pk && !(uf && uf[0] == '1'); /* packed: the per-SNP pass reads 2 bits per genotype */
   int G = std::min(nchrom, GD_DEFAULT_GROUPS);
   if (const char *eg = getenv("GD_GROUPS")) G = std::max(1, std::min(std::min(nchrom, GD_MAX_GROUPS), atoi(eg))); /* diagnostics */
   std::vector<int> cuts(G + 1);
@@ -373,12 +452,20 @@ static int fet_scan_locked(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, cons
       amax = std::max<int64_t>(amax, pl.h[c].alen);
       mx = std::max<int64_t>(mx, std::max(pl.h[c].alen, pl.h[c].blen) + 1);
     }
-    const unsigned gxb = (unsigned)std::min<int64_t>((mx + 4095) / 4096, std::max(1, 8192 / nc));
-    hipLaunchKernelGGL(k_bounds, dim3(gxb, nc, 2), dim3(256), 0, sm, d_ch + c0, apos, bpos, wsize, wstep, lo_a,
-                       hi_a, lo_b, flags);
-    const unsigned gxs = (unsigned)std::min<int64_t>((amax + 255) / 256, std::max(1, 8192 / nc));
-    hipLaunchKernelGGL(k_snp_fet, dim3(gxs, nc), dim3(256), 0, sm, d_ch + c0, avals, bvals, binom,
-                       ctx->lut_hdr, ctx->lut, snp, fused ? 1 : 0);
+    if (pk) {
+      if ((st = gd_packed_bounds_launch(d_ch + c0, nc, d_roff + c0, pk->rowpos, max_rows, wsize, wstep, lo_a, hi_a,
+                                        lo_b, flags, sm)) ||
+          (st = gd_packed_snp_fet_launch(d_ch + c0, nc, d_woff + 2 * c0, pk->acodes, pk->bcodes, max_rows, binom,
+                                         ctx->lut_hdr, ctx->lut, snp, sm)))
+        return fail(st, "packed pass launch failed");
+    } else {
+      const unsigned gxb = (unsigned)std::min<int64_t>((mx + 4095) / 4096, std::max(1, 8192 / nc));
+      hipLaunchKernelGGL(k_bounds, dim3(gxb, nc, 2), dim3(256), 0, sm, d_ch + c0, apos, bpos, wsize, wstep, lo_a,
+                         hi_a, lo_b, flags);
+      const unsigned gxs = (unsigned)std::min<int64_t>((amax + 255) / 256, std::max(1, 8192 / nc));
+      hipLaunchKernelGGL(k_snp_fet, dim3(gxs, nc), dim3(256), 0, sm, d_ch + c0, avals, bvals, binom,
+                         ctx->lut_hdr, ctx->lut, snp, fused ? 1 : 0);
+    }
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(ctx->gev[g], sm));
   }
@@ -514,7 +601,7 @@ static int host_scan(const double *avals, const double *bvals, const int *apos, 
 static int css_scan_locked(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, const double *avals,
                            const double *bvals, const int32_t *apos, const int32_t *bpos, int wsize, int wstep,
                            int treshold, int runs, int drosophila, int mds, int window_set, double *scores, double *p,
-                           hipStream_t s);
+                           hipStream_t s, const PackedIn *pk = nullptr);
 
 /* several chromosomes from host memory in one device scan: H2D of the inputs and of
  * the caller's outputs (kept at uncomputed windows), the batched scan, D2H */
@@ -648,14 +735,20 @@ extern "C" int gd_fet_compute(const double *avals, const double *bvals, const in
 }
 
 /* --------------------------------------------------------------- CSS scan */
+/* pk != NULL: a packed batch (count metric only) */
 static int css_scan_locked(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, const double *avals,
                            const double *bvals, const int32_t *apos, const int32_t *bpos, int wsize, int wstep,
                            int treshold, int runs, int drosophila, int mds, int window_set, double *scores, double *p,
-                           hipStream_t s) {
+                           hipStream_t s, const PackedIn *pk) {
   if (drosophila != 0 && drosophila != 1) return fail(GD_ERR_ARG, "drosophila must be 0 or 1");
   if (mds < 0 || mds > 2) return fail(GD_ERR_ARG, "mds must be 0 (classical), 1 (SMACOF) or 2 (SMACOF + classical)");
+  if (pk && drosophila)
+    return fail(GD_ERR_ARG, "packed tracks carry genotype codes, not the drosophila allele frequencies");
   ScanPlan pl;
-  int st = make_plan(chroms, nchrom, wsize, wstep, window_set, &pl);
+  std::vector<int64_t> row_off, word_off;
+  int64_t max_rows = 1;
+  int st = pk ? make_plan_packed(*pk, nchrom, wsize, wstep, window_set, &pl, &row_off, &word_off, &max_rows)
+              : make_plan(chroms, nchrom, wsize, wstep, window_set, &pl);
   if (st) return st;
   for (float &m : g_stage_ms) m = 0.f;
   if (pl.wtotal == 0) return GD_OK;
@@ -663,6 +756,7 @@ static int css_scan_locked(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, cons
   /* pass 1: population sizes + window bounds; the CSS kernels are specialised on
    * m = asize + bsize and the bit planes are sized by it, so read the sizes back */
   Carve cv{nullptr};
+  int64_t *d_roff = nullptr, *d_woff = nullptr; /* packed batches: row and word offsets */
   auto layout1 = [&](Carve &k, gd_chrom_dev **d_ch, unsigned **flags, int32_t **lo_a, int32_t **hi_a,
                      int32_t **lo_b) {
     *d_ch = k.take<gd_chrom_dev>(nchrom);
@@ -670,6 +764,10 @@ static int css_scan_locked(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, cons
     *lo_a = k.take<int32_t>(pl.wtotal);
     *hi_a = k.take<int32_t>(pl.wtotal);
     *lo_b = k.take<int32_t>(pl.wtotal);
+    if (pk) {
+      d_roff = k.take<int64_t>(nchrom);
+      d_woff = k.take<int64_t>(2 * (size_t)nchrom);
+    }
   };
   gd_chrom_dev *d_ch;
   unsigned *flags;
@@ -684,8 +782,14 @@ static int css_scan_locked(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, cons
   HIP_TRY(hipMemcpyAsync(d_ch, pl.h.data(), sizeof(gd_chrom_dev) * nchrom, hipMemcpyHostToDevice, s));
   HIP_TRY(hipMemsetAsync(flags, 0, 16 * sizeof(unsigned), s));
   HIP_TRY(hipEventRecord(ctx->ev[0], s));
-  hipLaunchKernelGGL(k_popsize, dim3(nchrom), dim3(64), 0, s, d_ch, apos, bpos, flags);
-  {
+  if (pk) {
+    HIP_TRY(hipMemcpyAsync(d_roff, row_off.data(), sizeof(int64_t) * nchrom, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(d_woff, word_off.data(), sizeof(int64_t) * 2 * nchrom, hipMemcpyHostToDevice, s));
+    if ((st = gd_packed_bounds_launch(d_ch, nchrom, d_roff, pk->rowpos, max_rows, wsize, wstep, lo_a, hi_a, lo_b,
+                                      flags, s)))
+      return fail(st, "packed bounds launch failed");
+  } else {
+    hipLaunchKernelGGL(k_popsize, dim3(nchrom), dim3(64), 0, s, d_ch, apos, bpos, flags);
     const int64_t mx = std::max(pl.max_alen, pl.max_blen) + 1;
     const unsigned gx = (unsigned)std::min<int64_t>((mx + 4095) / 4096, std::max(1, 8192 / nchrom));
     hipLaunchKernelGGL(k_bounds, dim3(gx, nchrom, 2), dim3(256), 0, s, d_ch, apos, bpos, wsize, wstep, lo_a,
@@ -762,8 +866,9 @@ static int css_scan_locked(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, cons
   HIP_TRY(hipMemsetAsync(planes, 0, sizeof(uint32_t) * std::max<int64_t>(words, 1), s));
   if (perms) HIP_TRY(hipMemsetAsync(status, 0, pl.wtotal, s));
   HIP_TRY(hipEventRecord(ctx->ev[1], s));
-  st = gd_css_launch(mp, drosophila, mds, d_ch, nchrom, d_pl, planes, lo_a, hi_a, lo_b, avals, bvals, pl.wtotal,
-                     max_words, treshold, runs, scores, p, xbuf, status, flags, s, ctx->ev[2]);
+  st = gd_css_launch(mp, drosophila, mds, d_ch, nchrom, d_pl, planes, lo_a, hi_a, lo_b, avals, bvals, d_woff,
+                     pk ? pk->acodes : nullptr, pk ? pk->bcodes : nullptr, pl.wtotal, max_words, treshold, runs,
+                     scores, p, xbuf, status, flags, s, ctx->ev[2]);
   if (st) return fail(st, "CSS kernel launch failed");
   HIP_TRY(hipEventRecord(ctx->ev[3], s));
   HIP_TRY(hipMemcpyAsync(ctx->h_flags, flags, 16 * sizeof(unsigned), hipMemcpyDeviceToHost, s));
@@ -837,6 +942,114 @@ extern "C" int gd_css_compute(const double *avals, const double *bvals, const in
 /* ------------------------------------------------------------- utilities */
 extern "C" void gd_set_seed(uint64_t seed) { g_seed.store(seed); }
 extern "C" uint64_t gd_get_seed(void) { return g_seed.load(); }
+/* ------------------------------------------------------------ packed tracks */
+extern "C" int gd_fet_scan_packed_device(gd_ctx *ctx, const gd_pchrom *chroms, int nchrom, const uint64_t *acodes,
+                                         const uint64_t *bcodes, const int32_t *rowpos, int wsize, int wstep,
+                                         double perc, int mode, int window_set, double *scores, double *stddev,
+                                         void *hip_stream) {
+  if (!ctx) return fail(GD_ERR_ARG, "null context");
+  std::lock_guard<std::mutex> g(ctx->mu);
+  const PackedIn pk{chroms, acodes, bcodes, rowpos};
+  return fet_scan_locked(ctx, nullptr, nchrom, nullptr, nullptr, nullptr, nullptr, wsize, wstep, perc, mode,
+                         window_set, scores, stddev, (hipStream_t)hip_stream, &pk);
+}
+
+extern "C" int gd_css_scan_packed_device(gd_ctx *ctx, const gd_pchrom *chroms, int nchrom, const uint64_t *acodes,
+                                         const uint64_t *bcodes, const int32_t *rowpos, int wsize, int wstep,
+                                         int treshold, int runs, int mds, int window_set, double *scores, double *p,
+                                         void *hip_stream) {
+  if (!ctx) return fail(GD_ERR_ARG, "null context");
+  std::lock_guard<std::mutex> g(ctx->mu);
+  const PackedIn pk{chroms, acodes, bcodes, rowpos};
+  return css_scan_locked(ctx, nullptr, nchrom, nullptr, nullptr, nullptr, nullptr, wsize, wstep, treshold, runs, 0,
+                         mds, window_set, scores, p, (hipStream_t)hip_stream, &pk);
+}
+
+/* a packed batch from host memory: H2D of the codes, positions and the caller's outputs
+ * (kept at uncomputed windows), the device scan, D2H */
+template <class Run>
+static int packed_host(const gd_pchrom *chroms, int nchrom, const uint64_t *acodes, const uint64_t *bcodes,
+                       const int32_t *rowpos, int wstep, double *out0, double *out1, Run run) {
+  if (nchrom < 0 || (nchrom > 0 && !chroms)) return fail(GD_ERR_ARG, "bad chromosome list");
+  if (wstep <= 0) return fail(GD_ERR_ARG, "wsize and wstep must be positive");
+  int64_t nrow = 0, nwa = 0, nwb = 0, nw = 0;
+  for (int c = 0; c < nchrom; ++c) {
+    const gd_pchrom &q = chroms[c];
+    if (q.nrows < 0 || q.row_off < 0 || q.a_word < 0 || q.b_word < 0 || q.w_out < 0)
+      return fail(GD_ERR_ARG, "negative extent");
+    if (q.nrows > 0 && (q.asize <= 0 || q.bsize <= 0)) return fail(GD_ERR_SIZE, "empty population");
+    nrow = std::max<int64_t>(nrow, q.row_off + q.nrows);
+    nwa = std::max<int64_t>(nwa, q.a_word + (int64_t)q.nrows * GD_PACK_WORDS(std::max(q.asize, 0)));
+    nwb = std::max<int64_t>(nwb, q.b_word + (int64_t)q.nrows * GD_PACK_WORDS(std::max(q.bsize, 0)));
+    if (q.regend > 0) nw = std::max<int64_t>(nw, q.w_out + q.regend / wstep);
+  }
+  if (nrow == 0 || nw == 0) return GD_OK;
+  if (!acodes || !bcodes || !rowpos || !out0 || !out1) return fail(GD_ERR_ARG, "null buffer");
+  int st;
+  gd_ctx *ctx = default_ctx(&st);
+  if (!ctx) return st ? st : fail(GD_ERR_HIP, "no HIP device available");
+  std::lock_guard<std::mutex> g(ctx->mu);
+  HIP_TRY(hipSetDevice(ctx->device));
+  const size_t need = sizeof(uint64_t) * (nwa + nwb) + sizeof(int32_t) * nrow + 2 * sizeof(double) * nw + 1024;
+  if ((st = grow(&ctx->io, &ctx->io_cap, need))) return st;
+  Carve k{ctx->io};
+  uint64_t *ca = k.take<uint64_t>(nwa), *cb = k.take<uint64_t>(nwb);
+  int32_t *rp = k.take<int32_t>(nrow);
+  double *o0 = k.take<double>(nw), *o1 = k.take<double>(nw);
+  hipStream_t s = ctx->stream;
+  HIP_TRY(hipMemcpyAsync(ca, acodes, sizeof(uint64_t) * nwa, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(cb, bcodes, sizeof(uint64_t) * nwb, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(rp, rowpos, sizeof(int32_t) * nrow, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(o0, out0, sizeof(double) * nw, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(o1, out1, sizeof(double) * nw, hipMemcpyHostToDevice, s));
+  const PackedIn pk{chroms, ca, cb, rp};
+  if ((st = run(ctx, pk, o0, o1, s))) return st;
+  HIP_TRY(hipMemcpyAsync(out0, o0, sizeof(double) * nw, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(out1, o1, sizeof(double) * nw, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  return GD_OK;
+}
+
+extern "C" int gd_fet_scan_packed_host(const gd_pchrom *chroms, int nchrom, const uint64_t *acodes,
+                                       const uint64_t *bcodes, const int32_t *rowpos, int wsize, int wstep,
+                                       double perc, int mode, int window_set, double *scores, double *stddev) {
+  return packed_host(chroms, nchrom, acodes, bcodes, rowpos, wstep, scores, stddev,
+                     [&](gd_ctx *ctx, const PackedIn &pk, double *o0, double *o1, hipStream_t s) {
+                       return fet_scan_locked(ctx, nullptr, nchrom, nullptr, nullptr, nullptr, nullptr, wsize, wstep,
+                                              perc, mode, window_set, o0, o1, s, &pk);
+                     });
+}
+
+extern "C" int gd_css_scan_packed_host(const gd_pchrom *chroms, int nchrom, const uint64_t *acodes,
+                                       const uint64_t *bcodes, const int32_t *rowpos, int wsize, int wstep,
+                                       int treshold, int runs, int mds, int window_set, double *scores, double *p) {
+  return packed_host(chroms, nchrom, acodes, bcodes, rowpos, wstep, scores, p,
+                     [&](gd_ctx *ctx, const PackedIn &pk, double *o0, double *o1, hipStream_t s) {
+                       return css_scan_locked(ctx, nullptr, nchrom, nullptr, nullptr, nullptr, nullptr, wsize, wstep,
+                                              treshold, runs, 0, mds, window_set, o0, o1, s, &pk);
+                     });
+}
+
+extern "C" int gd_pack_chrom_device(const double *avals, const double *bvals, const int32_t *apos,
+                                    const int32_t *bpos, int asize, int bsize, int nrows, uint64_t *acodes,
+                                    uint64_t *bcodes, int32_t *rowpos, void *hip_stream) {
+  if (asize <= 0 || bsize <= 0 || nrows < 0) return fail(GD_ERR_ARG, "population sizes must be positive");
+  if (nrows == 0) return GD_OK;
+  int st;
+  gd_ctx *ctx = default_ctx(&st);
+  if (!ctx) return st ? st : fail(GD_ERR_HIP, "no HIP device available");
+  std::lock_guard<std::mutex> g(ctx->mu);
+  hipStream_t s = hip_stream ? (hipStream_t)hip_stream : ctx->stream;
+  HIP_TRY(hipMemsetAsync(ctx->h_flags_dev, 0, sizeof(unsigned), s));
+  if ((st = gd_pack_device_launch(avals, bvals, apos, bpos, asize, bsize, nrows, acodes, bcodes, rowpos,
+                                  ctx->h_flags_dev, s)))
+    return fail(st, "pack kernel launch failed");
+  HIP_TRY(hipMemcpyAsync(ctx->h_flags, ctx->h_flags_dev, sizeof(unsigned), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  if (ctx->h_flags[0]) return fail(GD_ERR_ARG, "a value is not a genotype code or a row's positions differ");
+  return GD_OK;
+}
+
 extern "C" int gd_set_fet_mode(int mode) {
   if (mode != GD_FET_REFERENCE && mode != GD_FET_EXACT)
     return fail(GD_ERR_ARG, "FET mode must be GD_FET_REFERENCE (0) or GD_FET_EXACT (1)");

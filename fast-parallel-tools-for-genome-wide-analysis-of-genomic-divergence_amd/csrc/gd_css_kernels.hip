@@ -1098,7 +1098,10 @@ __global__ void __launch_bounds__((CssShape<MP, G>::NT), CSS_MDS_WAVES(MP))
   }
 }
 
-/* the other stages of a scan (gd_css_perm.hip, gd_css_smacof.hip) */
+/* the other stages of a scan (gd_css_perm.hip, gd_css_smacof.hip, gd_packed.hip) */
+int gd_packed_css_planes_launch(const gd_chrom_dev *d_ch, int nchrom, const gd_css_planes *d_pl,
+                                const int64_t *word_off, const uint64_t *acodes, const uint64_t *bcodes,
+                                int64_t max_rows_words, uint32_t *planes, hipStream_t s);
 int gd_css_perm_launch(int mp, const gd_chrom_dev *d_ch, int nchrom, const double *xbuf, const uint8_t *status,
                        int64_t wtotal, int treshold, int runs, double *p, unsigned *wq, hipStream_t s);
 int gd_css_smacof_launch(int mp, bool freq, const gd_chrom_dev *d_ch, int nchrom, const gd_css_planes *d_pl,
@@ -1136,16 +1139,22 @@ static int launch_tier(const gd_chrom_dev *d_ch, int nchrom, const gd_css_planes
  *   mds 1: k_css_smacof from drand48 starts
  *   mds 2: the classical stage, then k_css_smacof from its coordinates (xbuf)
  * xbuf/status carry the coordinates between stages when runs > 0 or mds == 2. */
+/* acodes != NULL: a packed batch; its bit planes come from the codes (never irregular,
+ * rows always aligned, so the literal per-SNP path and the raw values are never read) */
 int gd_css_launch(int mp, int drosophila, int mds, const gd_chrom_dev *d_ch, int nchrom, const gd_css_planes *d_pl,
                   uint32_t *planes, const int32_t *lo_a, const int32_t *hi_a, const int32_t *lo_b,
-                  const double *avals, const double *bvals, int64_t wtotal, int64_t max_rows_words, int treshold,
-                  int runs, double *scores, double *p, double *xbuf, uint8_t *status, unsigned *flags,
-                  hipStream_t s, hipEvent_t ev_perm) {
+                  const double *avals, const double *bvals, const int64_t *word_off, const uint64_t *acodes,
+                  const uint64_t *bcodes, int64_t wtotal, int64_t max_rows_words, int treshold, int runs,
+                  double *scores, double *p, double *xbuf, uint8_t *status, unsigned *flags, hipStream_t s,
+                  hipEvent_t ev_perm) {
   const bool perms = runs > 0 && treshold > 0;
   const int want_x1 = (perms || mds == 2) ? 1 : 0; /* coordinates out of the classical stage */
   const char *fl = getenv("GD_CSS_FORCE_LITERAL"); /* diagnostics: per-SNP predicate for every window */
-  const int force_literal = (fl && fl[0] == '1') ? 1 : 0;
-  if (!drosophila) {
+  const int force_literal = (fl && fl[0] == '1' && !acodes) ? 1 : 0;
+  if (acodes) {
+    const int st = gd_packed_css_planes_launch(d_ch, nchrom, d_pl, word_off, acodes, bcodes, max_rows_words, planes, s);
+    if (st) return st;
+  } else if (!drosophila) {
     const unsigned gx = (unsigned)std::min<int64_t>((max_rows_words * 8 + 255) / 256, std::max(1, 16384 / nchrom));
     hipLaunchKernelGGL(k_css_pack, dim3(std::max(1u, gx), nchrom, 2), dim3(256), 0, s, d_ch, d_pl, avals, bvals,
                        planes);

@@ -43,6 +43,8 @@ EXPORTS = (
     "gd_tabular_read", "gd_tabular_free", "gd_tabular_rows", "gd_tabular_nseq", "gd_tabular_seqid",
     "gd_tabular_copy",
     "gd_fet_region_limit", "gd_css_fdr_threshold", "gd_css_top_limit", "gd_merge_regions",
+    "gd_pack_shape", "gd_pack_chrom", "gd_pack_chrom_device", "gd_fet_scan_packed_device",
+    "gd_css_scan_packed_device", "gd_fet_scan_packed_host", "gd_css_scan_packed_host",
 )
 
 
@@ -57,6 +59,15 @@ class Chrom(C.Structure):
         ("a_off", C.c_int64), ("b_off", C.c_int64),
         ("alen", C.c_int32), ("blen", C.c_int32),
         ("regend", C.c_int32), ("pad_", C.c_int32),
+        ("w_out", C.c_int64), ("seed", C.c_uint64),
+    ]
+
+
+class PChrom(C.Structure):
+    """gd_pchrom (include/gdscan.h): one chromosome of a packed batch."""
+    _fields_ = [
+        ("row_off", C.c_int64), ("a_word", C.c_int64), ("b_word", C.c_int64),
+        ("nrows", C.c_int32), ("asize", C.c_int32), ("bsize", C.c_int32), ("regend", C.c_int32),
         ("w_out", C.c_int64), ("seed", C.c_uint64),
     ]
 
@@ -140,6 +151,19 @@ def _load() -> C.CDLL:
     lib.gd_merge_regions.argtypes = [vp, vp, vp, vp, i64, i32, C.c_double, i64, vp, i32, vp, vp, pi64, pi64, vp]
     for fn in ("gd_tabular_nseq", "gd_tabular_copy", "gd_fet_region_limit", "gd_css_fdr_threshold",
                "gd_css_top_limit", "gd_merge_regions"):
+        getattr(lib, fn).restype = C.c_int
+    lib.gd_pack_shape.argtypes = [ip, ip, i32, i32, ip, ip, ip]
+    lib.gd_pack_chrom.argtypes = [dp, dp, ip, ip, i32, i32, i32, vp, vp, vp]
+    lib.gd_pack_chrom_device.argtypes = [vp, vp, vp, vp, i32, i32, i32, vp, vp, vp, vp]
+    lib.gd_fet_scan_packed_device.argtypes = [vp, C.POINTER(PChrom), i32, vp, vp, vp, i32, i32, C.c_double, i32, i32,
+                                              vp, vp, vp]
+    lib.gd_css_scan_packed_device.argtypes = [vp, C.POINTER(PChrom), i32, vp, vp, vp, i32, i32, i32, i32, i32, i32,
+                                              vp, vp, vp]
+    lib.gd_fet_scan_packed_host.argtypes = [C.POINTER(PChrom), i32, vp, vp, vp, i32, i32, C.c_double, i32, i32, dp,
+                                            dp]
+    lib.gd_css_scan_packed_host.argtypes = [C.POINTER(PChrom), i32, vp, vp, vp, i32, i32, i32, i32, i32, i32, dp, dp]
+    for fn in ("gd_pack_shape", "gd_pack_chrom", "gd_pack_chrom_device", "gd_fet_scan_packed_device",
+               "gd_css_scan_packed_device", "gd_fet_scan_packed_host", "gd_css_scan_packed_host"):
         getattr(lib, fn).restype = C.c_int
     for fn in ("gd_gtrack_nseq", "gd_gtrack_copy", "gd_write_tabular", "gd_format_py2_float"):
         getattr(lib, fn).restype = C.c_int

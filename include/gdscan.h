@@ -139,6 +139,56 @@ int gd_css_scan_host_batch_ex(const gd_chrom *chroms, int nchrom, const double *
                               const int *apos, const int *bpos, int wsize, int wstep, int treshold, int runs,
                               int drosophila, int mds, int window_set, double *scores, double *p);
 
+/* ---- packed genotype tracks (second half) ----
+ * The four values VCFConvert.py:8-17 writes, as 2-bit codes; one position per SNP row
+ * (the reference layout repeats it per individual).  Population P of a chromosome with
+ * nrows rows is nrows x GD_PACK_WORDS(Psize) uint64 words: individual k of row r sits in
+ * bits 2 (k mod 32) of word r * GD_PACK_WORDS(Psize) + k / 32; padding codes are 0.
+ * A packed chromosome scans exactly like its expanded form (individual k of row r at
+ * element r * size, both populations at the row's position): same windows, same
+ * scores, same bootstrap / permutation streams. */
+#define GD_PACK_WORDS(size) (((size) + 31) / 32)
+#define GD_CODE_HET 0u     /* value 0 (heterozygous / other call) */
+#define GD_CODE_MAJOR 1u   /* value 3 (homozygous major) */
+#define GD_CODE_MINOR 2u   /* value -3 (homozygous minor) */
+#define GD_CODE_MISSING 3u /* value -10000 (missing) */
+typedef struct gd_pchrom {
+  int64_t row_off;        /* first row of this chromosome in rowpos */
+  int64_t a_word, b_word; /* first word of its rows in acodes / bcodes */
+  int32_t nrows, asize, bsize;
+  int32_t regend;         /* region end; windows are [w*wstep, w*wstep+wsize] */
+  int64_t w_out;          /* index in scores/stddev|p of window 0 */
+  uint64_t seed;
+} gd_pchrom;
+/* get_population_size() of both tracks (comparative.c:25-34) and the number of rows both
+ * hold whole (min(alen / asize, blen / bsize)); host memory */
+int gd_pack_shape(const int *apos, const int *bpos, int alen, int blen, int *asize, int *bsize, int *nrows);
+/* packs nrows rows (host memory; outputs hold nrows * GD_PACK_WORDS(size) words and nrows
+ * positions).  GD_ERR_ARG when a value is not one of the four codes or an individual's
+ * position (A or B) differs from its row's (apos[r * asize]): such tracks keep the
+ * reference layout (gd_*_scan_*). */
+int gd_pack_chrom(const double *avals, const double *bvals, const int *apos, const int *bpos, int asize, int bsize,
+                  int nrows, uint64_t *acodes, uint64_t *bcodes, int32_t *rowpos);
+/* the same on the device (device pointers; a reference-layout track already in HBM) */
+int gd_pack_chrom_device(const double *avals, const double *bvals, const int32_t *apos, const int32_t *bpos,
+                         int asize, int bsize, int nrows, uint64_t *acodes, uint64_t *bcodes, int32_t *rowpos,
+                         void *hip_stream);
+/* scans of packed batches: device pointers (except `chroms`) ... */
+int gd_fet_scan_packed_device(gd_ctx *ctx, const gd_pchrom *chroms, int nchrom, const uint64_t *acodes,
+                              const uint64_t *bcodes, const int32_t *rowpos, int wsize, int wstep, double perc,
+                              int mode, int window_set, double *scores, double *stddev, void *hip_stream);
+/* CSS: count metric only (drosophila = 0); mds 0 / 1 / 2 as gd_css_scan_host_ex */
+int gd_css_scan_packed_device(gd_ctx *ctx, const gd_pchrom *chroms, int nchrom, const uint64_t *acodes,
+                              const uint64_t *bcodes, const int32_t *rowpos, int wsize, int wstep, int treshold,
+                              int runs, int mds, int window_set, double *scores, double *p, void *hip_stream);
+/* ... and from host memory (the codes cross PCIe: 2 bits per genotype + 4 B per row) */
+int gd_fet_scan_packed_host(const gd_pchrom *chroms, int nchrom, const uint64_t *acodes, const uint64_t *bcodes,
+                            const int32_t *rowpos, int wsize, int wstep, double perc, int mode, int window_set,
+                            double *scores, double *stddev);
+int gd_css_scan_packed_host(const gd_pchrom *chroms, int nchrom, const uint64_t *acodes, const uint64_t *bcodes,
+                            const int32_t *rowpos, int wsize, int wstep, int treshold, int runs, int mds,
+                            int window_set, double *scores, double *p);
+
 /* ---- region filters after the scan ----
  * A track is the list of windows a tool's tabular file holds (score != 0), in file
  * order.  Array arguments may be host or device memory; ctx NULL selects the process-wide
