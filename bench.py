@@ -68,6 +68,7 @@ def parse():
     ap.add_argument("--cpu-chroms", type=int, default=20, help="chromosomes in the CPU-baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-css", action="store_true", help="skip the CSS leg")
+    ap.add_argument("--no-extra", action="store_true", help="skip the region-filter and packed-track legs")
     ap.add_argument("--css-steps", type=int, default=3)
     ap.add_argument("--css-cpu-snps", type=int, default=150_000, help="SNPs in the CSS CPU-baseline sample")
     return ap.parse_args()
@@ -474,9 +475,10 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(args)
 
-    out["regions"] = regions_run(args, scores, stddev, chroms, nch, rank, world, dev)
-    out["packed"] = packed_run(args, lib, _lib, check, ctx, stream, dev, avals, bvals, apos, bpos, chroms, nch,
-                               scores, stddev)
+    if not args.no_extra:
+        out["regions"] = regions_run(args, scores, stddev, chroms, nch, rank, world, dev)
+        out["packed"] = packed_run(args, lib, _lib, check, ctx, stream, dev, avals, bvals, apos, bpos, chroms, nch,
+                                   scores, stddev)
 
     if not args.no_css:
         pv = torch.zeros_like(scores)

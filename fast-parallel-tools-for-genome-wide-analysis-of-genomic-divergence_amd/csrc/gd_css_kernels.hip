@@ -754,7 +754,9 @@ __global__ void __launch_bounds__((CssShape<MP, G>::NT), CSS_MDS_WAVES(MP))
      * handled in blocks of 8; a block dead in every column part (v, w and x are 0
      * left of k) is skipped by a uniform branch. */
     if constexpr (G == 1 && MP <= 40) {
+#ifndef GD_CSS_SKIP_TRIDIAG
       HhStatic<MP, 0>::run(A, m, i, ii, tid, row, s_row, s_v, s_w, s_d, s_e, s_tau, s_red);
+#endif
     } else if constexpr (G == 2 && MP <= CSS_STATIC_G2_MAX) {
       HhStaticG<MP, G, 0>::run(A, m, i, h, ii, tid, row, lead, s_row, s_v, s_w, s_d, s_e, s_tau, s_red);
     } else
@@ -892,7 +894,11 @@ __global__ void __launch_bounds__((CssShape<MP, G>::NT), CSS_MDS_WAVES(MP))
       const int hh = tid >> 5, j = tid & 31;
       const int target = m - 1 - hh; /* ascending index of the eigenvalue */
       double l = glo, u = ghi;
+#ifdef GD_CSS_SKIP_BISECT
+      for (int it = 0; it < 0; ++it) {
+#else
       for (int it = 0; it < 80; ++it) {
+#endif
         const double x = l + (u - l) * ((double)(j + 1) * (1.0 / 33.0));
         /* d and e^2 are padded to a multiple of 4 with decoupled entries above the
          * spectrum, so the unrolled groups need no tail */
@@ -981,7 +987,11 @@ __global__ void __launch_bounds__((CssShape<MP, G>::NT), CSS_MDS_WAVES(MP))
       }
     }
     double y1 = 0.0, y2 = 0.0;
+#ifdef GD_CSS_SKIP_INVIT
+    for (int itn = 0; itn < 0; ++itn) {
+#else
     for (int itn = 0; itn < 2; ++itn) {
+#endif
       __syncthreads();
       if (tid < 2) {
         double *y = s_y[tid];
@@ -1058,7 +1068,11 @@ __global__ void __launch_bounds__((CssShape<MP, G>::NT), CSS_MDS_WAVES(MP))
     /* ---- back-transformation y <- H_0 H_1 ... H_{m-3} y; v_k sits in column k,
      * i.e. in part k / CP of the row */
 #pragma unroll
+#ifdef GD_CSS_SKIP_BACK
+    for (int k = -1; k >= 0; --k) {
+#else
     for (int k = MP - 3; k >= 0; --k) {
+#endif
       if (k <= m - 3) {
         constexpr int dummy = 0;
         (void)dummy;

@@ -483,7 +483,11 @@ __global__ void __launch_bounds__(FW_WPB *FW_TPW)
   const int m = n - idx;
 
   /* ---- A2. the window's top-KTOP scores in ascending order (sh_top[wl][rank - base]) ---- */
+#ifdef GD_FET_NORANK
+  if (false) { /* diagnostics: ranking cost */
+#else
   if (fast) {
+#endif
     const double *S = sh_span + (sh_row[wl] - span0);
     int nan = 0;
     if (n <= FW_TPW * 8) {

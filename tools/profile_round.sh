@@ -12,11 +12,11 @@ timeout -k 10 420 python bench.py > $O/bench.json 2> $O/bench.err &&
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/ktrace -o run --output-format csv -- \
     python3 bench.py --steps 5 --warmup 1 --no-cpu > $O/ktrace_bench.json 2> $O/ktrace.err &&
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $O/pmc_fetch -o run --output-format csv -- \
-    python3 bench.py --steps 2 --warmup 1 --no-cpu --no-css > $O/pmc_fetch.json 2> $O/pmc_fetch.err &&
+    python3 bench.py --steps 2 --warmup 1 --no-cpu --no-css --no-extra > $O/pmc_fetch.json 2> $O/pmc_fetch.err &&
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d $O/pmc_write -o run --output-format csv -- \
-    python3 bench.py --steps 2 --warmup 1 --no-cpu --no-css > $O/pmc_write.json 2> $O/pmc_write.err &&
+    python3 bench.py --steps 2 --warmup 1 --no-cpu --no-css --no-extra > $O/pmc_write.json 2> $O/pmc_write.err &&
 timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES SQ_INSTS_SALU SQ_INSTS_LDS -d $O/pmc_valu -o run --output-format csv -- \
-    python3 bench.py --steps 2 --warmup 1 --no-cpu --no-css > $O/pmc_valu.json 2> $O/pmc_valu.err &&
+    python3 bench.py --steps 2 --warmup 1 --no-cpu --no-css --no-extra > $O/pmc_valu.json 2> $O/pmc_valu.err &&
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $O/pmc_css_fetch -o run --output-format csv -- \
     python3 bench.py --steps 1 --warmup 0 --no-cpu --css-steps 1 > $O/pmc_css.json 2> $O/pmc_css.err
 echo "profile_round exit $?"
