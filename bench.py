@@ -48,6 +48,7 @@ FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 vector spec; ubench: ~31
 PROFILE_ROUND = "r02"
 TRAFFIC_FILE = ROOT / "profiles" / f"{PROFILE_ROUND}_fet_traffic.json"
 VALU_FILE = ROOT / "profiles" / f"{PROFILE_ROUND}_fet_valu.json"
+CSS_VALU_FILE = ROOT / "profiles" / f"{PROFILE_ROUND}_css_valu.json"
 # VALU issue peak: 256 CUs x 4 SIMDs, one wave64 VALU instruction per 4 cycles per SIMD
 # at the 2.4 GHz max clock (MI355X_MICROARCH.md) = 614.4 G wave-instructions/s
 VALU_PEAK_GINSTS = 256 * 4 * 2.4 / 4
@@ -523,6 +524,17 @@ def main():
                          "kernel": "k_css_pack + k_css_mds (HIP events)", "kernel_ms": kms,
                          "alg_flops_per_window": flops / windows},
         }
+        if CSS_VALU_FILE.exists():
+            # what binds the MDS kernel: VALU issue -- per-window serial phases (Householder
+            # steps, Sturm bisection, inverse iteration, back-transformation) on a wave whose
+            # lanes hold the matrix rows (40 of 64 busy at m = 40)
+            cv = json.loads(CSS_VALU_FILE.read_text())
+            if cv.get("config") == [nch, nsnp, a, b]:
+                gi = cv["valu_wave_insts_per_scan"] / (kms * 1e-3) / 1e9
+                out["css"]["roofline"]["valu"] = {
+                    "bound": "valu-issue", "achieved": gi, "peak": VALU_PEAK_GINSTS, "unit": "G wave-insts/s",
+                    "frac": gi / VALU_PEAK_GINSTS, "insts_per_window": cv["valu_wave_insts_per_scan"] / windows,
+                    "source": f"{CSS_VALU_FILE.relative_to(ROOT)} ({cv['method']})"}
         if rank == 0 and world == 1 and not args.no_cpu:
             out["css"]["cpu_baseline"] = css_cpu_baseline(args)
         # the per-GPU shapes of configs[3] (40+40, runs=0) and configs[4] (40+40, mcT=10,

@@ -17,6 +17,8 @@ timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d $O/pmc_write -o run --output-for
     python3 bench.py --steps 2 --warmup 1 --no-cpu --no-css --no-extra > $O/pmc_write.json 2> $O/pmc_write.err &&
 timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES SQ_INSTS_SALU SQ_INSTS_LDS -d $O/pmc_valu -o run --output-format csv -- \
     python3 bench.py --steps 2 --warmup 1 --no-cpu --no-css --no-extra > $O/pmc_valu.json 2> $O/pmc_valu.err &&
+timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES -d $O/pmc_css_valu -o run --output-format csv -- \
+    python3 bench.py --steps 1 --warmup 0 --no-cpu --css-steps 1 --no-extra > $O/pmc_css_valu.json 2> $O/pmc_css_valu.err &&
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $O/pmc_css_fetch -o run --output-format csv -- \
     python3 bench.py --steps 1 --warmup 0 --no-cpu --css-steps 1 > $O/pmc_css.json 2> $O/pmc_css.err
 echo "profile_round exit $?"

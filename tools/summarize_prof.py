@@ -84,6 +84,17 @@ valu_doc = {
 }
 (dst / f"{R}_fet_valu.json").write_text(json.dumps(valu_doc, indent=1) + "\n")
 
+# CSS (C3 shape): VALU wave-instructions per call of the bit-plane pass and the m = 40 MDS kernel
+cval, ncv = counters(src / "pmc_css_valu", "SQ_INSTS_VALU")
+mds = [k for k in cval if k.startswith("k_css_mds<40")]
+css_doc = None
+if mds and ncv.get("k_css_pack", 0):
+    per_call = cval[mds[0]] / ncv[mds[0]] + cval["k_css_pack"] / ncv["k_css_pack"]
+    css_doc = {"config": traffic["config"], "valu_wave_insts_per_scan": per_call,
+               "method": "rocprofv3 --pmc SQ_INSTS_VALU over k_css_pack + k_css_mds<40, 1> (wave-instructions "
+                         "per call = per C3 scan)"}
+    (dst / f"{R}_css_valu.json").write_text(json.dumps(css_doc, indent=1) + "\n")
+
 rows = list(csv.DictReader(open(stats)))
 lines = [f"# {R} profile summary", "", "Command: `rocprofv3 --kernel-trace --stats -- python3 bench.py --steps 5 "
          "--warmup 1 --no-cpu` (FET + CSS legs), PMC passes separate (tools/profile_round.sh).", "",
