@@ -20,5 +20,5 @@ timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES SQ_INSTS_SALU SQ_INSTS_
 timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES -d $O/pmc_css_valu -o run --output-format csv -- \
     python3 bench.py --steps 1 --warmup 0 --no-cpu --css-steps 1 --no-extra > $O/pmc_css_valu.json 2> $O/pmc_css_valu.err &&
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $O/pmc_css_fetch -o run --output-format csv -- \
-    python3 bench.py --steps 1 --warmup 0 --no-cpu --css-steps 1 > $O/pmc_css.json 2> $O/pmc_css.err
+    python3 bench.py --steps 1 --warmup 0 --no-cpu --css-steps 1 --no-extra > $O/pmc_css.json 2> $O/pmc_css.err
 echo "profile_round exit $?"
