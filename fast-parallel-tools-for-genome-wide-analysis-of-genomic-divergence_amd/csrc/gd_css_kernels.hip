@@ -63,7 +63,14 @@ __device__ unsigned long long g_css_prof[8];
 #define CSS_BISECT_TOL 1e-9 /* bisection stops at this fraction of the spectral bound */
 #endif
 #ifndef CSS_MDS_WAVES
-#define CSS_MDS_WAVES(MP) ((MP) <= 24 ? 5 : (MP) <= 40 ? 4 : (MP) <= 64 ? 2 : (MP) <= 96 ? 3 : 2)
+#ifndef CSS_MDS_WAVES_G2
+#define CSS_MDS_WAVES_G2 3 /* waves per SIMD of the 80- and 96-individual tiers (diagnostic override) */
+#endif
+#ifndef CSS_G80
+#define CSS_G80 1 /* lanes per row of the 80-individual tier (2 measured 7 % slower) */
+#endif
+#define CSS_MDS_WAVES(MP, G) \
+  ((MP) <= 24 ? 5 : (MP) <= 40 ? 4 : (MP) <= 64 || (G) == 1 ? 2 : (MP) <= 96 ? CSS_MDS_WAVES_G2 : 2)
 #endif
 
 namespace {
@@ -136,6 +143,16 @@ __device__ __forceinline__ double readlane_f64(double v, int lane) {
   const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), lane);
   return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
 }
+/* The lane id, produced by an asm statement so the compiler can neither hoist it nor
+ * carry it across the unrolled Householder steps: the row index and the LDS addresses
+ * derived from it are rebuilt per step (a few VALU) instead of being kept live through
+ * all of them, which at the register limit got them spilled to scratch and reloaded
+ * on the serial chain of every step. */
+__device__ __forceinline__ int css_lane_now() {
+  int l;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+  return l;
+}
 struct OpSum {
   static __device__ __forceinline__ double id() { return 0.0; }
   static __device__ __forceinline__ double op(double x, double y) { return x + y; }
@@ -185,7 +202,7 @@ __device__ __forceinline__ double block_reduce(double v, double *red) {
     return v;
   } else {
     __syncthreads();
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    if (css_lane_now() == 0) red[__builtin_amdgcn_readfirstlane(threadIdx.x) >> 6] = v;
     __syncthreads();
     double s = red[0];
 #pragma unroll
@@ -202,9 +219,10 @@ __device__ __forceinline__ void block_sum2(double &a, double &b, double *red) {
   wave_sum2(a, b);
   if constexpr (NW > 1) {
     __syncthreads();
-    if ((threadIdx.x & 63) == 0) {
-      red[threadIdx.x >> 6] = a;
-      red[NW + (threadIdx.x >> 6)] = b;
+    if (css_lane_now() == 0) {
+      const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x) >> 6;
+      red[wv] = a;
+      red[NW + wv] = b;
     }
     __syncthreads();
     double sa = red[0], sb = red[NW];
@@ -330,9 +348,10 @@ __device__ __forceinline__ double pair_sum(double x) {
  * tiers up to 40 individuals): block skipping, the dead-column stash and the reads
  * of x, d_K and A e_{K+1} all resolve to fixed registers -- no per-column selects. */
 template <int MP, int K>
-__device__ __forceinline__ void hh_step_static(double (&A)[MP], int m, int i, int ii, int tid, bool row,
-                                               double *s_row, double *s_v, double *s_w, double *s_d, double *s_e,
-                                               double *s_tau, double *s_red) {
+__device__ __forceinline__ void hh_step_static(double (&A)[MP], int m, double *s_row, double *s_v, double *s_w,
+                                               double *s_d, double *s_e, double *s_tau) {
+  const int i = css_lane_now(), tid = i, ii = i < MP ? i : MP - 1; /* one wave: row = lane */
+  const bool row = i < m;
   __syncthreads();
   if (i == K) {
 #pragma unroll
@@ -415,18 +434,17 @@ __device__ __forceinline__ void hh_step_static(double (&A)[MP], int m, int i, in
 
 template <int MP, int K>
 struct HhStatic {
-  static __device__ __forceinline__ void run(double (&A)[MP], int m, int i, int ii, int tid, bool row, double *s_row,
-                                             double *s_v, double *s_w, double *s_d, double *s_e, double *s_tau,
-                                             double *s_red) {
+  static __device__ __forceinline__ void run(double (&A)[MP], int m, double *s_row, double *s_v, double *s_w,
+                                             double *s_d, double *s_e, double *s_tau) {
     if ((K & 7) == 0 && K >= m) return; /* exits only at block boundaries (see above) */
-    hh_step_static<MP, K>(A, m, i, ii, tid, row, s_row, s_v, s_w, s_d, s_e, s_tau, s_red);
-    HhStatic<MP, K + 1>::run(A, m, i, ii, tid, row, s_row, s_v, s_w, s_d, s_e, s_tau, s_red);
+    hh_step_static<MP, K>(A, m, s_row, s_v, s_w, s_d, s_e, s_tau);
+    HhStatic<MP, K + 1>::run(A, m, s_row, s_v, s_w, s_d, s_e, s_tau);
   }
 };
 template <int MP>
 struct HhStatic<MP, MP> {
-  static __device__ __forceinline__ void run(double (&)[MP], int, int, int, int, bool, double *, double *, double *,
-                                             double *, double *, double *, double *) {}
+  static __device__ __forceinline__ void run(double (&)[MP], int, double *, double *, double *, double *, double *,
+                                             double *) {}
 };
 
 /* The compile-time-K step for the two-lanes-per-row tiers (G = 2): lane part h holds
@@ -451,14 +469,24 @@ __device__ __forceinline__ void hh_publish_part(const double (&A)[MP / G], doubl
 }
 
 template <int MP, int G, int K>
-__device__ __forceinline__ void hh_step_static_g(double (&A)[MP / G], int m, int i, int h, int ii, int tid,
-                                                 bool row, bool lead, double *s_row, double *s_v, double *s_w,
-                                                 double *s_d, double *s_e, double *s_tau, double *s_red) {
+__device__ __forceinline__ void hh_step_static_g(double (&A)[MP / G], int m, int wave, double *s_row, double *s_v,
+                                                 double *s_w, double *s_d, double *s_e, double *s_tau,
+                                                 double *s_red) {
   constexpr int CP = MP / G, NW = CssShape<MP, G>::NW;
+  const int lane = css_lane_now(), tid = wave * 64 + lane;
+  const int i = tid / G, h = tid % G, ii = i < MP ? i : MP - 1;
+  const bool row = i < m, lead = h == 0;
   const int c0 = h * CP;
-  __syncthreads();
+  /* No barrier ahead of the publish: every read of s_row by step K-1 happened before
+   * its v/w barrier, which every wave has passed by now.  The reduction slots alternate
+   * between two banks by step parity, so their writes need no barrier of their own.
+   * (Step MP-2 reads s_row after its publish without a later barrier: step MP-1 keeps it.) */
+  if constexpr (K == 0 || K == MP - 1) __syncthreads();
+  double *red = s_red + (K & 1) * (2 * NW + 2);
   if (i == K) {
-    if (h == 0)
+    if constexpr (G == 1)
+      hh_publish_part<MP, G, K, 0>(A, s_row, s_d);
+    else if (h == 0)
       hh_publish_part<MP, G, K, 0>(A, s_row, s_d);
     else
       hh_publish_part<MP, G, K, 1>(A, s_row, s_d);
@@ -492,11 +520,23 @@ __device__ __forceinline__ void hh_step_static_g(double (&A)[MP / G], int m, int
     static_assert(NW > 1, "block_sum2 synchronises the slots only across waves");
     double sigma = lead ? xi * xi : 0.0, q = (lead && i > K && row) ? s_row[ii] * praw : 0.0;
     if (lead && i == K + 1) {
-      s_red[2 * NW] = praw;
-      s_red[2 * NW + 1] = ak1;
+      red[2 * NW] = praw;
+      red[2 * NW + 1] = ak1;
     }
-    block_sum2<NW>(sigma, q, s_red);
-    const double pr1 = s_red[2 * NW], a11 = s_red[2 * NW + 1];
+    wave_sum2(sigma, q);
+    if (lane == 0) {
+      red[wave] = sigma;
+      red[NW + wave] = q;
+    }
+    __syncthreads();
+    sigma = red[0];
+    q = red[NW];
+#pragma unroll
+    for (int k = 1; k < NW; ++k) {
+      sigma += red[k];
+      q += red[NW + k];
+    }
+    const double pr1 = red[2 * NW], a11 = red[2 * NW + 1];
     double tau = 0.0, beta = alpha, scale = 0.0;
     if (sigma != 0.0) {
       beta = -copysign(sqrt(alpha * alpha + sigma), alpha);
@@ -536,22 +576,21 @@ __device__ __forceinline__ void hh_step_static_g(double (&A)[MP / G], int m, int
 
 template <int MP, int G, int K>
 struct HhStaticG {
-  static __device__ __forceinline__ void run(double (&A)[MP / G], int m, int i, int h, int ii, int tid, bool row,
-                                             bool lead, double *s_row, double *s_v, double *s_w, double *s_d,
-                                             double *s_e, double *s_tau, double *s_red) {
+  static __device__ __forceinline__ void run(double (&A)[MP / G], int m, int wave, double *s_row, double *s_v,
+                                             double *s_w, double *s_d, double *s_e, double *s_tau, double *s_red) {
     if ((K & 7) == 0 && K >= m) return;
-    hh_step_static_g<MP, G, K>(A, m, i, h, ii, tid, row, lead, s_row, s_v, s_w, s_d, s_e, s_tau, s_red);
-    HhStaticG<MP, G, K + 1>::run(A, m, i, h, ii, tid, row, lead, s_row, s_v, s_w, s_d, s_e, s_tau, s_red);
+    hh_step_static_g<MP, G, K>(A, m, wave, s_row, s_v, s_w, s_d, s_e, s_tau, s_red);
+    HhStaticG<MP, G, K + 1>::run(A, m, wave, s_row, s_v, s_w, s_d, s_e, s_tau, s_red);
   }
 };
 template <int MP, int G>
 struct HhStaticG<MP, G, MP> {
-  static __device__ __forceinline__ void run(double (&)[MP / G], int, int, int, int, int, bool, bool, double *,
-                                             double *, double *, double *, double *, double *, double *) {}
+  static __device__ __forceinline__ void run(double (&)[MP / G], int, int, double *, double *, double *, double *,
+                                             double *, double *, double *) {}
 };
 
 template <int MP, int G>
-__global__ void __launch_bounds__((CssShape<MP, G>::NT), CSS_MDS_WAVES(MP))
+__global__ void __launch_bounds__((CssShape<MP, G>::NT), CSS_MDS_WAVES(MP, G))
     k_css_mds(const gd_chrom_dev *ch, int nchrom, const gd_css_planes *pl, const uint32_t *planes,
               const int32_t *lo_a_, const int32_t *hi_a_, const int32_t *lo_b_, const double *avals,
               const double *bvals, int64_t wtotal, int want_x, int force_literal, double *scores, double *pvals,
@@ -570,7 +609,8 @@ __global__ void __launch_bounds__((CssShape<MP, G>::NT), CSS_MDS_WAVES(MP))
   __shared__ double s_x[2 * MP];
   __shared__ int s_tr[MP];
   __shared__ double s_lam[2];
-  __shared__ double s_red[2 * NW + 2]; /* block sums; [2NW], [2NW+1]: row K+1 in a Householder step */
+  __shared__ double s_red[2 * (2 * NW + 2)]; /* block sums; [2NW], [2NW+1]: row K+1 in a Householder step
+                                                (two banks, alternating by step in the G = 2 steps) */
 
   const int tid = threadIdx.x;
   const int i = tid / G, h = tid % G; /* row, column part */
@@ -755,10 +795,11 @@ __global__ void __launch_bounds__((CssShape<MP, G>::NT), CSS_MDS_WAVES(MP))
      * left of k) is skipped by a uniform branch. */
     if constexpr (G == 1 && MP <= 40) {
 #ifndef GD_CSS_SKIP_TRIDIAG
-      HhStatic<MP, 0>::run(A, m, i, ii, tid, row, s_row, s_v, s_w, s_d, s_e, s_tau, s_red);
+      HhStatic<MP, 0>::run(A, m, s_row, s_v, s_w, s_d, s_e, s_tau);
 #endif
-    } else if constexpr (G == 2 && MP <= CSS_STATIC_G2_MAX) {
-      HhStaticG<MP, G, 0>::run(A, m, i, h, ii, tid, row, lead, s_row, s_v, s_w, s_d, s_e, s_tau, s_red);
+    } else if constexpr ((G == 2 || MP > 64) && MP <= CSS_STATIC_G2_MAX) {
+      HhStaticG<MP, G, 0>::run(A, m, __builtin_amdgcn_readfirstlane(tid >> 6), s_row, s_v, s_w, s_d, s_e, s_tau,
+                               s_red);
     } else
     for (int k = 0; k < m; ++k) {
       __syncthreads();
@@ -1205,7 +1246,7 @@ int gd_css_launch(int mp, int drosophila, int mds, const gd_chrom_dev *d_ch, int
         CSS_TIER(24, 1)
         CSS_TIER(40, 1)
         CSS_TIER(64, 1)
-        CSS_TIER(80, 2)
+        CSS_TIER(80, CSS_G80)
         CSS_TIER(96, 2)
         CSS_TIER(128, 2)
         default:

@@ -61,7 +61,10 @@ template <int MP>
 struct PermShape {
   static constexpr int TRI = MP * (MP + 1) / 2 + 1; /* packed triangle + padding row + zero */
   static constexpr int HALF = MP / 2;               /* largest smaller-group size */
-  static constexpr int NWV = MP <= 64 ? 4 : 2;
+#ifndef PERM_NWV_LARGE
+#define PERM_NWV_LARGE 2 /* waves per workgroup above 64 individuals */
+#endif
+  static constexpr int NWV = MP <= 64 ? 4 : PERM_NWV_LARGE;
   static constexpr int NT = 64 * NWV;
 };
 
@@ -196,8 +199,13 @@ __device__ __forceinline__ void fy_exact(uint8_t *col, uint64_t x, int m, const 
 
 }  // namespace
 
+#ifdef PERM_WAVES_PER_SIMD /* diagnostic: register-allocation target */
+#define PERM_WPE __attribute__((amdgpu_waves_per_eu(PERM_WAVES_PER_SIMD, PERM_WAVES_PER_SIMD)))
+#else
+#define PERM_WPE
+#endif
 template <int MP>
-__global__ void __launch_bounds__(PermShape<MP>::NT)
+__global__ void __launch_bounds__(PermShape<MP>::NT) PERM_WPE
     k_css_perm(const gd_chrom_dev *ch, int nchrom, const double *xbuf, const uint8_t *status, int64_t wtotal,
                int treshold, int runs, double *pvals, unsigned *wq) {
   constexpr int TRI = PermShape<MP>::TRI, NWV = PermShape<MP>::NWV, NT = PermShape<MP>::NT, P = 64 * NWV;
