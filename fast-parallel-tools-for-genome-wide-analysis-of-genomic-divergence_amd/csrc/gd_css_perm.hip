@@ -36,6 +36,24 @@
  * loops as ~100 live VGPRs. */
 #define PERM_OPAQUE(x) asm volatile("" : "+v"(x))
 
+#ifdef GD_PERM_PROFILE
+/* diagnostics build only: shader-clock cycles per phase summed over workgroups (thread 0) */
+#include <cstdio>
+__device__ unsigned long long g_perm_prof[8];
+#define PERM_PROF_INIT uint64_t prof_t = __builtin_readcyclecounter()
+#define PERM_PROF(ph)                                                  \
+  do {                                                                 \
+    if (threadIdx.x == 0) {                                            \
+      const uint64_t t_ = __builtin_readcyclecounter();               \
+      atomicAdd(&g_perm_prof[ph], (unsigned long long)(t_ - prof_t)); \
+      prof_t = t_;                                                     \
+    }                                                                  \
+  } while (0)
+#else
+#define PERM_PROF_INIT
+#define PERM_PROF(ph)
+#endif
+
 namespace {
 
 __device__ __forceinline__ int perm_chrom_of(const gd_chrom_dev *ch, int nchrom, int64_t w) {
@@ -80,34 +98,74 @@ __device__ __forceinline__ double s_pair(const double *S, uint32_t x, uint32_t t
 }
 
 /* css() of the track array in column `lane` of sig (byte k at sig[k*64 + lane]).
- * The pairs of the smaller group are visited in 8x8 blocks of members (runtime
- * block loops, unrolled blocks), which bounds both the code and the loads in flight. */
+ * The consecutive within-group pairs (css.c:627-642) are summed first, in track
+ * order; the smaller group G is collected as a bit set on the way and then written
+ * back over the head of the column in ascending order (the column is dead after
+ * the score).  With the members ascending, pair (u < v) sits at T(x_v) + x_u with no
+ * compare, and the between-group term becomes a function of the SET G alone, so
+ * every permutation that keeps the groups' sets gets the observed value bit for bit.
+ * Pairs are visited in 8x8 blocks of members (runtime block loops, unrolled blocks),
+ * which bounds both the code and the loads in flight. */
 template <int MP>
-__device__ __forceinline__ double perm_score(const double *S, const double *R, const uint8_t *sig, int lane, int a,
-                                             int b, double inva, double invb) {
+__device__ __forceinline__ double perm_score(const double *S, const double *R, uint8_t *sig, int lane, int a, int b,
+                                             double inva, double invb) {
   constexpr int NB = (PermShape<MP>::HALF + 7) / 8;
   const int m = a + b;
   const int g = a <= b ? a : b, off = a <= b ? 0 : a;
   PERM_OPAQUE(lane);
-  const uint8_t *col = sig + lane;
-  /* member k of the smaller group, padded with the zero individual MP */
-  auto member = [&](int k) -> uint32_t { return k < g ? (uint32_t)col[(off + k) * 64] : (uint32_t)MP; };
+  uint8_t *col = sig + lane;
+  const char *Sb = reinterpret_cast<const char *>(S);
+  /* consecutive pairs inside each group, and G as a bit set */
+  double wa = 0.0, wb = 0.0;
+  uint64_t lo = 0, hi = 0;
+  auto add_member = [&](uint32_t x) {
+    lo |= x < 64 ? 1ull << (x & 63u) : 0ull;
+    if constexpr (MP > 64) hi |= x >= 64 ? 1ull << (x & 63u) : 0ull;
+  };
+  uint32_t prev = col[0], tprev = tri8(prev);
+  if (off == 0 && g > 0) add_member(prev);
+#pragma unroll 4
+  for (int k = 1; k < m; ++k) {
+    const uint32_t cur = col[k * 64], tcur = tri8(cur);
+    const double e = s_pair(S, prev, tprev, cur, tcur);
+    if (k < a) wa += e;
+    if (k > a) wb += e;
+    if (k >= off && k < off + g) add_member(cur);
+    prev = cur;
+    tprev = tcur;
+  }
+  /* the members, ascending, over bytes 0 .. g-1 of the column */
+#pragma unroll 4
+  for (int k = 0; k < g; ++k) {
+    uint32_t x;
+    if (MP <= 64 || lo != 0) {
+      x = (uint32_t)__builtin_ctzll(lo);
+      lo &= lo - 1;
+    } else {
+      x = 64u + (uint32_t)__builtin_ctzll(hi);
+      hi &= hi - 1;
+    }
+    col[k * 64] = (uint8_t)x;
+  }
+  /* member k of G, padded with the zero individual MP (the largest index) */
+  auto member = [&](int k) -> uint32_t { return k < g ? (uint32_t)col[k * 64] : (uint32_t)MP; };
+  auto s_at = [&](uint32_t off8) { return *reinterpret_cast<const double *>(Sb + off8); };
   double sr = 0.0, q0 = 0.0, q1 = 0.0, q2 = 0.0, q3 = 0.0;
 #pragma unroll 1
   for (int K = 0; K < NB; ++K) {
-    uint32_t xk[8], tk[8];
+    uint32_t xk8[8], tk[8];
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
-      xk[u] = member(8 * K + u);
-      tk[u] = tri8(xk[u]);
+      const uint32_t x = member(8 * K + u);
+      sr += R[x];
+      xk8[u] = x << 3;
+      tk[u] = tri8(x);
     }
-#pragma unroll
-    for (int u = 0; u < 8; ++u) sr += R[xk[u]];
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
 #pragma unroll
       for (int v = u + 1; v < 8; ++v) {
-        const double e = s_pair(S, xk[u], tk[u], xk[v], tk[v]);
+        const double e = s_at(tk[v] + xk8[u]); /* x_u < x_v */
         if ((u + v) & 1)
           q0 += e;
         else
@@ -117,17 +175,14 @@ __device__ __forceinline__ double perm_score(const double *S, const double *R, c
     }
 #pragma unroll 1
     for (int L = K + 1; L < NB; ++L) {
-      uint32_t xl[8], tl[8];
+      uint32_t tl[8];
 #pragma unroll
-      for (int v = 0; v < 8; ++v) {
-        xl[v] = member(8 * L + v);
-        tl[v] = tri8(xl[v]);
-      }
+      for (int v = 0; v < 8; ++v) tl[v] = tri8(member(8 * L + v));
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
 #pragma unroll
         for (int v = 0; v < 8; ++v) {
-          const double e = s_pair(S, xk[u], tk[u], xl[v], tl[v]);
+          const double e = s_at(tl[v] + xk8[u]); /* every member of block K < every member of block L */
           if (v & 1)
             q3 += e;
           else
@@ -136,18 +191,6 @@ __device__ __forceinline__ double perm_score(const double *S, const double *R, c
         asm volatile("" ::: "memory");
       }
     }
-  }
-  /* consecutive pairs inside each group (css.c:627-642) */
-  double wa = 0.0, wb = 0.0;
-  uint32_t prev = col[0], tprev = tri8(prev);
-#pragma unroll 4
-  for (int k = 1; k < m; ++k) {
-    const uint32_t cur = col[k * 64], tcur = tri8(cur);
-    const double e = s_pair(S, prev, tprev, cur, tcur);
-    if (k < a) wa += e;
-    if (k > a) wb += e;
-    prev = cur;
-    tprev = tcur;
   }
   const double bet = sr - 2.0 * ((q0 + q1) + (q2 + q3));
   return bet / (double)(a * b) - (double)(a + b) * (wa * inva + wb * invb);
@@ -223,6 +266,7 @@ __global__ void __launch_bounds__(PermShape<MP>::NT) PERM_WPE
   double *s_x = reinterpret_cast<double *>(s_sig); /* X staging, dead before the draws */
   uint8_t *my_sig = s_sig + wave * SIG;
 
+  PERM_PROF_INIT;
   for (;;) {
     __syncthreads();
     if (tid == 0) s_w = (int64_t)atomicAdd(wq, 1u);
@@ -264,6 +308,7 @@ __global__ void __launch_bounds__(PermShape<MP>::NT) PERM_WPE
     sig_identity(my_sig, m, lane);
     __syncthreads();
     const double obs = perm_score<MP>(s_S, s_R, my_sig, lane, a, b, inva, invb);
+    PERM_PROF(0);
 
     uint64_t base = gd_window_state(d.seed, GD_STREAM_CSS, wl);
     const gd_affine Jq = gd_lcg_jump((uint64_t)tid * (uint64_t)m1), JP = gd_lcg_jump((uint64_t)P * (uint64_t)m1);
@@ -301,6 +346,7 @@ __global__ void __launch_bounds__(PermShape<MP>::NT) PERM_WPE
         base = gd_affine_apply(JP, base);
       }
       __syncthreads();
+      PERM_PROF(1);
 
       /* 2. F_q = F_{q-1} o sigma_q, one wave after the other; lane i owns rows i and i + 64 */
       for (int v = 0; v < NWV; ++v) {
@@ -339,8 +385,13 @@ __global__ void __launch_bounds__(PermShape<MP>::NT) PERM_WPE
         __syncthreads();
       }
 
+      PERM_PROF(2);
       /* 3. scores of the P permuted track arrays, 4. in-order hit count */
       const double sc = perm_score<MP>(s_S, s_R, my_sig, lane, a, b, inva, invb);
+#ifdef GD_PERM_PROFILE
+      __syncthreads();
+      PERM_PROF(3);
+#endif
       const int valid = min(P, runs - nsc);
       const uint64_t H = __ballot(tid < valid && sc >= obs);
       if (lane == 0) s_hit[wave] = H;
@@ -362,6 +413,7 @@ __global__ void __launch_bounds__(PermShape<MP>::NT) PERM_WPE
         }
       }
     }
+    PERM_PROF(4);
     if (tid == 0) pvals[d.w_out + wl] = (hits + 1) * 1.0 / (nsc + 1);
   }
 }
@@ -377,6 +429,22 @@ static int launch_perm(const gd_chrom_dev *d_ch, int nchrom, const double *xbuf,
 
 int gd_css_perm_launch(int mp, const gd_chrom_dev *d_ch, int nchrom, const double *xbuf, const uint8_t *status,
                        int64_t wtotal, int treshold, int runs, double *p, unsigned *wq, hipStream_t s) {
+#ifdef GD_PERM_PROFILE
+  {
+    static const unsigned long long z[8] = {0};
+    (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_perm_prof), z, sizeof z, 0, hipMemcpyHostToDevice, s);
+  }
+  struct Dump {
+    hipStream_t s;
+    ~Dump() {
+      unsigned long long h[8];
+      (void)hipStreamSynchronize(s);
+      (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(g_perm_prof), sizeof h);
+      fprintf(stderr, "perm-prof cycles: setup %llu draws %llu compose %llu score %llu hits %llu\n", h[0], h[1], h[2],
+              h[3], h[4]);
+    }
+  } dump{s};
+#endif
   switch (mp) {
     case 24: return launch_perm<24>(d_ch, nchrom, xbuf, status, wtotal, treshold, runs, p, wq, s);
     case 40: return launch_perm<40>(d_ch, nchrom, xbuf, status, wtotal, treshold, runs, p, wq, s);
