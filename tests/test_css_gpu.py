@@ -47,10 +47,14 @@ def test_serial_window_set(oracle):
     assert np.array_equal(p, p_ref)
 
 
-@pytest.mark.parametrize("asize,bsize,treshold,runs", [(10, 10, 10, 300), (20, 20, 5, 100), (6, 9, 50, 1000)])
-def test_permutation_p_matches_oracle(oracle, asize, bsize, treshold, runs):
+@pytest.mark.parametrize("asize,bsize,treshold,runs,nsnp", [(10, 10, 10, 300, 15_000), (20, 20, 5, 100, 15_000),
+                                                            (6, 9, 50, 1000, 15_000), (40, 40, 10, 300, 3_000),
+                                                            (33, 31, 10, 200, 3_000)])
+def test_permutation_p_matches_oracle(oracle, asize, bsize, treshold, runs, nsnp):
+    """The C5 shape (40+40, the two-rows-per-lane composition and the 80-tier MDS
+    coordinates) included."""
     from gdscan import css
-    av, bv, ap, bp, regend = _synth(5, 15_000, asize, bsize)
+    av, bv, ap, bp, regend = _synth(5, nsnp, asize, bsize)
     s, p = css.scan(av, bv, ap, bp, regend, treshold=treshold, runs=runs, seed=77)
     s_ref, p_ref = oracle_css_scan(oracle, av, bv, ap, bp, regend, treshold=treshold, runs=runs, seed=77)
     _cmp_scores(s, s_ref)
@@ -60,11 +64,12 @@ def test_permutation_p_matches_oracle(oracle, asize, bsize, treshold, runs):
     assert np.all(p[~comp] == 0)
 
 
-def test_irregular_values_take_the_literal_path(oracle):
+@pytest.mark.parametrize("asize,bsize,nsnp", [(8, 8, 20_000), (40, 40, 3_000)])
+def test_irregular_values_take_the_literal_path(oracle, asize, bsize, nsnp):
     """Values outside {3,0,-3,-10000} (including NaN and huge values) follow the
     reference predicate (int)v_i * v_j == -9 with x86 cast semantics."""
     from gdscan import css
-    av, bv, ap, bp, regend = _synth(6, 20_000, 8, 8)
+    av, bv, ap, bp, regend = _synth(6, nsnp, asize, bsize)
     rng = np.random.default_rng(0)
     for arr in (av, bv):
         idx = rng.choice(len(arr), 400, replace=False)
