@@ -66,6 +66,9 @@ __device__ unsigned long long g_css_prof[8];
 #ifndef CSS_MDS_WAVES_G2
 #define CSS_MDS_WAVES_G2 3 /* waves per SIMD of the 80- and 96-individual tiers (diagnostic override) */
 #endif
+#ifndef CSS_T80
+#define CSS_T80 1 /* the 80-individual tier in one wave with an LDS tail (k_css_mds_t80) */
+#endif
 #ifndef CSS_G80
 #define CSS_G80 1 /* lanes per row of the 80-individual tier (2 measured 7 % slower) */
 #endif
@@ -278,10 +281,138 @@ __device__ __forceinline__ double css_score(const int *tracks, int a, int b, Dis
     bet += dist(tracks[ii], tracks[a + jj]);
   }
   /* consecutive pairs only (Q8), each pre-divided by its group's a^2 (a-1) */
-  if (t < a - 1) win = dist(tracks[t], tracks[t + 1]) / (double)(a * a * (a - 1));
-  if (t >= a && t < m - 1) win = dist(tracks[t], tracks[t + 1]) / (double)(b * b * (b - 1));
+  for (int k = t; k < m - 1; k += NT) {
+    if (k < a - 1) win += dist(tracks[k], tracks[k + 1]) / (double)(a * a * (a - 1));
+    if (k >= a) win += dist(tracks[k], tracks[k + 1]) / (double)(b * b * (b - 1));
+  }
   block_sum2<NW>(bet, win, red);
   return bet / (a * b) - (a + b) * win;
+}
+
+/* The two largest eigenvalues of T by 33-section bisection, one half-wave per
+ * eigenvalue (lanes 0..63 of one wave).  Sturm counts come from the sign changes of
+ * the leading principal minors p_k(x) (three-term recurrence, rescaled every 4
+ * steps): no division on the serial chain.  d (s_d) and e^2 (s_e2, e_{k-1}^2 at k,
+ * s_e2[0] = 0) are padded to a multiple of 4 with decoupled entries above the
+ * spectrum. */
+__device__ __forceinline__ void bisect_top2(int m, double glo, double ghi, double bis_tol, const double *s_d,
+                                            const double *s_e2, double *s_lam, int lane) {
+  const int m4 = (m + 3) & ~3;
+  const int hh = lane >> 5, j = lane & 31;
+  const int target = m - 1 - hh; /* ascending index of the eigenvalue */
+  double l = glo, u = ghi;
+#ifdef GD_CSS_SKIP_BISECT
+  for (int it = 0; it < 0; ++it) {
+#else
+  for (int it = 0; it < 80; ++it) {
+#endif
+    const double x = l + (u - l) * ((double)(j + 1) * (1.0 / 33.0));
+    /* d and e^2 are padded to a multiple of 4 with decoupled entries above the
+     * spectrum, so the unrolled groups need no tail */
+    double pm = 1.0, pc = 1.0;
+    int cnt = 0;
+    for (int k = 0; k < m4; k += 4) {
+      const double2 d01 = *reinterpret_cast<const double2 *>(s_d + k);
+      const double2 d23 = *reinterpret_cast<const double2 *>(s_d + k + 2);
+      const double2 e01 = *reinterpret_cast<const double2 *>(s_e2 + k);
+      const double2 e23 = *reinterpret_cast<const double2 *>(s_e2 + k + 2);
+      const double dk[4] = {d01.x, d01.y, d23.x, d23.y};
+      const double ek[4] = {e01.x, e01.y, e23.x, e23.y}; /* e_{k-1}^2, s_e2[0] = 0 */
+#pragma unroll
+      for (int uu = 0; uu < 4; ++uu) {
+        double pn = fma(dk[uu] - x, pc, -(ek[uu] * pm));
+        /* an exactly zero minor takes the sign opposite to its predecessor */
+        pn = (pn == 0.0) ? -pc * DBL_MIN : pn;
+        cnt += (int)((__double2hiint(pn) ^ __double2hiint(pc)) < 0);
+        pm = pc;
+        pc = pn;
+      }
+      const int ex = __builtin_amdgcn_frexp_exp(fmax(fabs(pm), fabs(pc)));
+      pm = __builtin_amdgcn_ldexp(pm, -ex);
+      pc = __builtin_amdgcn_ldexp(pc, -ex);
+    }
+    double nl = cnt <= target ? x : l;
+    double nu = cnt <= target ? u : x;
+    /* half-wave max / min: xor butterflies inside each 32-lane half */
+#pragma unroll
+    for (int o = 16; o >= 1; o >>= 1) {
+      nl = fmax(nl, __shfl_xor(nl, o));
+      nu = fmin(nu, __shfl_xor(nu, o));
+    }
+    const bool same = (nl == l && nu == u);
+    l = nl;
+    u = nu;
+    /* a shift within CSS_BISECT_TOL ||T|| is all inverse iteration needs (its two
+     * solves gain (shift error / gap)^2 on the eigenvector); the eigenvalue itself
+     * comes back to rounding as the Rayleigh quotient below */
+    const bool conv = same || (u - l) <= bis_tol;
+    if (__all(conv)) break;
+  }
+  if (j == 0) s_lam[hh] = 0.5 * (l + u);
+}
+
+/* eigenvector e of T (0: largest, 1: second): partial-pivot LU of T - lam_e I (U in
+ * s_lu[e], multipliers in s_x + e MP, pivots in s_piv[e]) and the start vector in
+ * s_y[e]; one lane.  The serial chain carries its running values in registers; LDS
+ * holds only read-once factors. */
+template <int MP>
+__device__ __forceinline__ void invit_factor(int m, int e, const double *s_d, const double *s_e, const double *s_lam,
+                                             double (*s_lu)[3][MP], double *s_x, uint8_t (*s_piv)[MP],
+                                             double (*s_y)[MP]) {
+  const double sig = s_lam[e];
+  double *U0 = s_lu[e][0], *U1 = s_lu[e][1], *U2 = s_lu[e][2];
+  double *ml = s_x + e * MP; /* elimination multipliers; s_x is free until X is formed */
+  uint8_t *pv = s_piv[e];
+  double cc0 = s_d[0] - sig, cc1 = m > 1 ? s_e[0] : 0.0;
+  for (int k = 0; k < m - 1; ++k) {
+    const double n0 = s_e[k], n1 = s_d[k + 1] - sig, n2 = (k + 2 < m) ? s_e[k + 1] : 0.0;
+    const bool sw = fabs(cc0) < fabs(n0);
+    const double pvt = sw ? n0 : cc0, oth = sw ? cc0 : n0;
+    const double t = (pvt != 0.0) ? oth * fast_rcp(pvt) : 0.0;
+    U0[k] = pvt;
+    U1[k] = sw ? n1 : cc1;
+    U2[k] = sw ? n2 : 0.0;
+    ml[k] = t;
+    pv[k] = sw;
+    const double nc0 = sw ? fma(-t, n1, cc1) : fma(-t, cc1, n1);
+    cc1 = sw ? -t * n2 : n2;
+    cc0 = nc0;
+  }
+  U0[m - 1] = cc0;
+  /* start vector: deterministic, not orthogonal to anything in practice */
+  for (int k = 0; k < m; ++k) {
+    const double f = (double)((k * 40503u + 977u * (unsigned)(e + 1)) & 1023u) / 1024.0;
+    s_y[e][k] = (e == 0 ? 1.0 : ((k & 1) ? -1.0 : 1.0)) * (0.5 + f);
+  }
+}
+
+/* one inverse-iteration solve (T - lam_e I) y = y with the factors of invit_factor, in
+ * place in s_y[e]; one lane */
+template <int MP>
+__device__ __forceinline__ void invit_solve(int m, int e, double (*s_lu)[3][MP], const double *s_x,
+                                            uint8_t (*s_piv)[MP], double (*s_y)[MP]) {
+  double *y = s_y[e];
+  const double *R0 = s_lu[e][0], *U1 = s_lu[e][1], *U2 = s_lu[e][2], *ml = s_x + e * MP;
+  const uint8_t *pv = s_piv[e];
+  double yk = y[0];
+  for (int k = 0; k < m - 1; ++k) {
+    double yn = y[k + 1];
+    if (pv[k]) {
+      const double t = yk;
+      yk = yn;
+      yn = t;
+    }
+    y[k] = yk;
+    yk = fma(-ml[k], yk, yn);
+  }
+  double z1 = yk * R0[m - 1], z2 = 0.0;
+  y[m - 1] = z1;
+  for (int k = m - 2; k >= 0; --k) {
+    const double z0 = (y[k] - U1[k] * z1 - U2[k] * z2) * R0[k];
+    y[k] = z0;
+    z2 = z1;
+    z1 = z0;
+  }
 }
 
 }  // namespace
@@ -928,95 +1059,16 @@ __global__ void __launch_bounds__((CssShape<MP, G>::NT), CSS_MDS_WAVES(MP, G))
       ghi += pad;
       if (tid >= m && tid < MP + 4) s_d[tid] = 2.0 * fabs(ghi) + 2.0 * fabs(glo) + 1.0;
     }
-    const int m4 = (m + 3) & ~3;
     const double bis_tol = CSS_BISECT_TOL * fmax(fabs(glo), fabs(ghi)) + DBL_MIN;
     __syncthreads();
-    if (tid < 64) {
-      const int hh = tid >> 5, j = tid & 31;
-      const int target = m - 1 - hh; /* ascending index of the eigenvalue */
-      double l = glo, u = ghi;
-#ifdef GD_CSS_SKIP_BISECT
-      for (int it = 0; it < 0; ++it) {
-#else
-      for (int it = 0; it < 80; ++it) {
-#endif
-        const double x = l + (u - l) * ((double)(j + 1) * (1.0 / 33.0));
-        /* d and e^2 are padded to a multiple of 4 with decoupled entries above the
-         * spectrum, so the unrolled groups need no tail */
-        double pm = 1.0, pc = 1.0;
-        int cnt = 0;
-        for (int k = 0; k < m4; k += 4) {
-          const double2 d01 = *reinterpret_cast<const double2 *>(s_d + k);
-          const double2 d23 = *reinterpret_cast<const double2 *>(s_d + k + 2);
-          const double2 e01 = *reinterpret_cast<const double2 *>(s_e2 + k);
-          const double2 e23 = *reinterpret_cast<const double2 *>(s_e2 + k + 2);
-          const double dk[4] = {d01.x, d01.y, d23.x, d23.y};
-          const double ek[4] = {e01.x, e01.y, e23.x, e23.y}; /* e_{k-1}^2, s_e2[0] = 0 */
-#pragma unroll
-          for (int uu = 0; uu < 4; ++uu) {
-            double pn = fma(dk[uu] - x, pc, -(ek[uu] * pm));
-            /* an exactly zero minor takes the sign opposite to its predecessor */
-            pn = (pn == 0.0) ? -pc * DBL_MIN : pn;
-            cnt += (int)((__double2hiint(pn) ^ __double2hiint(pc)) < 0);
-            pm = pc;
-            pc = pn;
-          }
-          const int ex = __builtin_amdgcn_frexp_exp(fmax(fabs(pm), fabs(pc)));
-          pm = __builtin_amdgcn_ldexp(pm, -ex);
-          pc = __builtin_amdgcn_ldexp(pc, -ex);
-        }
-        double nl = cnt <= target ? x : l;
-        double nu = cnt <= target ? u : x;
-        /* half-wave max / min: xor butterflies inside each 32-lane half */
-#pragma unroll
-        for (int o = 16; o >= 1; o >>= 1) {
-          nl = fmax(nl, __shfl_xor(nl, o));
-          nu = fmin(nu, __shfl_xor(nu, o));
-        }
-        const bool same = (nl == l && nu == u);
-        l = nl;
-        u = nu;
-        /* a shift within CSS_BISECT_TOL ||T|| is all inverse iteration needs (its two
-         * solves gain (shift error / gap)^2 on the eigenvector); the eigenvalue itself
-         * comes back to rounding as the Rayleigh quotient below */
-        const bool conv = same || (u - l) <= bis_tol;
-        if (__all(conv)) break;
-      }
-      if (j == 0) s_lam[hh] = 0.5 * (l + u);
-    }
+    if (tid < 64) bisect_top2(m, glo, ghi, bis_tol, s_d, s_e2, s_lam, tid);
     __syncthreads();
 
     CSS_PROF(3);
     /* ---- eigenvectors of T: two steps of inverse iteration with a partial-pivot
      * LU of T - lam I (thread 0: largest, thread 1: second).  The serial chains carry
      * their running values in registers; LDS holds only read-once factors. */
-    if (tid < 2) {
-      const double sig = s_lam[tid];
-      double *U0 = s_lu[tid][0], *U1 = s_lu[tid][1], *U2 = s_lu[tid][2];
-      double *ml = s_x + tid * MP; /* elimination multipliers; s_x is free until X is formed */
-      uint8_t *pv = s_piv[tid];
-      double cc0 = s_d[0] - sig, cc1 = m > 1 ? s_e[0] : 0.0;
-      for (int k = 0; k < m - 1; ++k) {
-        const double n0 = s_e[k], n1 = s_d[k + 1] - sig, n2 = (k + 2 < m) ? s_e[k + 1] : 0.0;
-        const bool sw = fabs(cc0) < fabs(n0);
-        const double pvt = sw ? n0 : cc0, oth = sw ? cc0 : n0;
-        const double t = (pvt != 0.0) ? oth * fast_rcp(pvt) : 0.0;
-        U0[k] = pvt;
-        U1[k] = sw ? n1 : cc1;
-        U2[k] = sw ? n2 : 0.0;
-        ml[k] = t;
-        pv[k] = sw;
-        const double nc0 = sw ? fma(-t, n1, cc1) : fma(-t, cc1, n1);
-        cc1 = sw ? -t * n2 : n2;
-        cc0 = nc0;
-      }
-      U0[m - 1] = cc0;
-      /* start vector: deterministic, not orthogonal to anything in practice */
-      for (int k = 0; k < m; ++k) {
-        const double f = (double)((k * 40503u + 977u * (unsigned)(tid + 1)) & 1023u) / 1024.0;
-        s_y[tid][k] = (tid == 0 ? 1.0 : ((k & 1) ? -1.0 : 1.0)) * (0.5 + f);
-      }
-    }
+    if (tid < 2) invit_factor<MP>(m, tid, s_d, s_e, s_lam, s_lu, s_x, s_piv, s_y);
     __syncthreads();
     if (tid < m) {
       /* reciprocal pivots, in parallel (zero pivots -> tiny) */
@@ -1034,30 +1086,7 @@ __global__ void __launch_bounds__((CssShape<MP, G>::NT), CSS_MDS_WAVES(MP, G))
     for (int itn = 0; itn < 2; ++itn) {
 #endif
       __syncthreads();
-      if (tid < 2) {
-        double *y = s_y[tid];
-        const double *R0 = s_lu[tid][0], *U1 = s_lu[tid][1], *U2 = s_lu[tid][2], *ml = s_x + tid * MP;
-        const uint8_t *pv = s_piv[tid];
-        double yk = y[0];
-        for (int k = 0; k < m - 1; ++k) {
-          double yn = y[k + 1];
-          if (pv[k]) {
-            const double t = yk;
-            yk = yn;
-            yn = t;
-          }
-          y[k] = yk;
-          yk = fma(-ml[k], yk, yn);
-        }
-        double z1 = yk * R0[m - 1], z2 = 0.0;
-        y[m - 1] = z1;
-        for (int k = m - 2; k >= 0; --k) {
-          const double z0 = (y[k] - U1[k] * z1 - U2[k] * z2) * R0[k];
-          y[k] = z0;
-          z2 = z1;
-          z1 = z0;
-        }
-      }
+      if (tid < 2) invit_solve<MP>(m, tid, s_lu, s_x, s_piv, s_y);
       __syncthreads();
       y1 = row ? s_y[0][ii] : 0.0;
       y2 = row ? s_y[1][ii] : 0.0;
@@ -1153,6 +1182,605 @@ __global__ void __launch_bounds__((CssShape<MP, G>::NT), CSS_MDS_WAVES(MP, G))
   }
 }
 
+/* ------------------------------------------------------------------------ */
+/* The 65..80-individual tier in ONE wave (k_css_mds_t80).  Rows 0..63 of the  */
+/* matrix live in the VGPRs of lanes 0..63 (80 columns each, as k_css_mds<MP, 1>); */
+/* rows 64..79 live in LDS, each worked by a quad of lanes over interleaved      */
+/* columns (lane 4r + q holds columns 4s + q of tail row r), so a column group    */
+/* dead for the main rows is dead for the tail too and both skip it by the same   */
+/* compile-time test.  One wave per window: no workgroup barriers, 2 waves per    */
+/* SIMD, 8 windows per CU (the two-wave layout ran 4, three barriers per step).   */
+/* ------------------------------------------------------------------------ */
+namespace {
+constexpr int T80 = 80, T80_MAIN = 64, T80_TS = 20; /* order, VGPR rows, tail columns per lane */
+
+/* sum over the 4 lanes of a quad (every lane gets the same bits) */
+__device__ __forceinline__ double quad_sum(double x) {
+  x += dpp64<0xB1, 0xF>(x, 0.0); /* quad_perm [1,0,3,2] */
+  return x + dpp64<0x4E, 0xF>(x, 0.0); /* quad_perm [2,3,0,1] */
+}
+
+/* One Householder step (hh_step_static) over the main rows and the LDS tail. */
+template <int K>
+__device__ __forceinline__ void t80_step(double (&A)[T80], int m, double *s_row, double *s_v, double *s_w,
+                                         double *s_d, double *s_e, double *s_tau, double (*s_tail)[T80]) {
+  constexpr int MP = T80;
+  const int i = css_lane_now(), tr = i >> 2, tq = i & 3, R = T80_MAIN + tr;
+  const bool row = i < m, trow = R < m;
+  __syncthreads();
+  if constexpr (K < T80_MAIN) {
+    if (i == K) {
+#pragma unroll
+      for (int jb = 0; jb < MP / 8; ++jb)
+        if (8 * jb + 7 >= K) {
+#pragma unroll
+          for (int u = 0; u < 8; u += 2) {
+            const int j = 8 * jb + u;
+            *reinterpret_cast<double2 *>(s_row + j) = make_double2(j > K ? A[j] : 0.0, j + 1 > K ? A[j + 1] : 0.0);
+          }
+        }
+      s_d[K] = A[K];
+    }
+  } else {
+    const double *src = s_tail[K - T80_MAIN];
+    s_row[i] = i > K ? src[i] : 0.0;
+    if (i + 64 < MP) s_row[i + 64] = i + 64 > K ? src[i + 64] : 0.0;
+    if (i == 0) s_d[K] = src[K];
+  }
+  __syncthreads();
+  if constexpr (K >= MP - 2) {
+    if (i == 0 && K == m - 2) s_e[K] = s_row[K + 1];
+    return;
+  } else {
+    /* K >= m - 2 below MP - 2: a no-op reflector on the zero padding (hh_step_static) */
+    const double xi = (i > K + 1 && row) ? s_row[i] : 0.0;
+    const double alpha = s_row[K + 1];
+    double p0 = 0, p1 = 0;
+#pragma unroll
+    for (int jb = 0; jb < MP / 8; ++jb) {
+      if (8 * jb + 7 > K) {
+#pragma unroll
+        for (int u = 0; u < 8; u += 2) {
+          if (8 * jb + u > K) p0 = fma(A[8 * jb + u], s_row[8 * jb + u], p0);
+          if (8 * jb + u + 1 > K) p1 = fma(A[8 * jb + u + 1], s_row[8 * jb + u + 1], p1);
+        }
+        CSS_PIN(p0);
+        CSS_PIN(p1);
+      }
+    }
+    const double ak1 = A[K + 1];
+    const double praw = p0 + p1;
+    /* the tail row over the live column groups (4s + 3 > K; s_row is 0 at j <= K) */
+    const double *trw = s_tail[tr];
+    double t0 = 0, t1 = 0;
+#pragma unroll
+    for (int s = 0; s < T80_TS; ++s) {
+      if (4 * s + 3 > K) {
+        const int j = 4 * s + tq;
+        if (s & 1)
+          t1 = fma(trw[j], s_row[j], t1);
+        else
+          t0 = fma(trw[j], s_row[j], t0);
+      }
+      if ((s & 3) == 3) {
+        CSS_PIN(t0);
+        CSS_PIN(t1);
+      }
+    }
+    const double pt = quad_sum(t0 + t1);
+    const double akt = trw[K + 1];
+    const double xr = (R > K + 1 && trow) ? s_row[R] : 0.0;
+    /* |x|^2 and r^T A r in one reduction (hh_step_static); a tail row counts once */
+    double sigma = xi * xi + (tq == 0 ? xr * xr : 0.0);
+    double q = ((i > K && row) ? s_row[i] : 0.0) * praw + ((tq == 0 && R > K && trow) ? s_row[R] * pt : 0.0);
+    wave_sum2(sigma, q);
+    double pr1, a11;
+    if constexpr (K + 1 < T80_MAIN) {
+      pr1 = readlane_f64(praw, K + 1);
+      a11 = readlane_f64(ak1, K + 1);
+    } else {
+      pr1 = readlane_f64(pt, 4 * (K + 1 - T80_MAIN));
+      a11 = readlane_f64(akt, 4 * (K + 1 - T80_MAIN));
+    }
+    double tau = 0.0, beta = alpha, scale = 0.0;
+    if (sigma != 0.0) {
+      beta = -copysign(sqrt(alpha * alpha + sigma), alpha);
+      const double r = fast_rcp(beta * (alpha - beta));
+      tau = -(alpha - beta) * (alpha - beta) * r;
+      scale = beta * r;
+    }
+    const double Kc = -0.5 * tau * (tau * scale * scale) * fma(beta, fma(beta, a11, -2.0 * pr1), q);
+    const double vi = (i == K + 1) ? 1.0 : xi * scale;
+    const double pi = (i > K && row) ? (tau * scale) * fma(-beta, ak1, praw) : 0.0;
+    const double wi = fma(Kc, vi, pi);
+    const double vt = (R == K + 1) ? 1.0 : xr * scale;
+    const double ptl = (R > K && trow) ? (tau * scale) * fma(-beta, akt, pt) : 0.0;
+    const double wt = fma(Kc, vt, ptl);
+    if (i == 0) {
+      s_e[K] = beta;
+      s_tau[K] = tau;
+    }
+    s_v[i] = vi;
+    s_w[i] = wi;
+    if (tq == 0) {
+      s_v[R] = vt;
+      s_w[R] = wt;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int jb = 0; jb < MP / 8; ++jb) {
+      if (8 * jb + 7 > K) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int j = 8 * jb + u;
+          if (j > K) A[j] = fma(-vi, s_w[j], fma(-wi, s_v[j], A[j]));
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) CSS_PIN(A[8 * jb + u]);
+      }
+    }
+    A[K] = vi; /* stash v_K in the dead column K */
+    double *tw = s_tail[tr];
+#pragma unroll
+    for (int s = 0; s < T80_TS; ++s) {
+      if (4 * s + 3 > K) {
+        const int j = 4 * s + tq;
+        tw[j] = fma(-vt, s_w[j], fma(-wt, s_v[j], tw[j]));
+      }
+    }
+    if (tq == (K & 3)) tw[K] = vt;
+  }
+}
+
+template <int K>
+struct T80Steps {
+  static __device__ __forceinline__ void run(double (&A)[T80], int m, double *s_row, double *s_v, double *s_w,
+                                             double *s_d, double *s_e, double *s_tau, double (*s_tail)[T80]) {
+    if ((K & 7) == 0 && K >= m) return; /* exits only at block boundaries (hh_step_static) */
+    t80_step<K>(A, m, s_row, s_v, s_w, s_d, s_e, s_tau, s_tail);
+    T80Steps<K + 1>::run(A, m, s_row, s_v, s_w, s_d, s_e, s_tau, s_tail);
+  }
+};
+template <>
+struct T80Steps<T80> {
+  static __device__ __forceinline__ void run(double (&)[T80], int, double *, double *, double *, double *, double *,
+                                             double *, double (*)[T80]) {}
+};
+}  // namespace
+
+__global__ void __launch_bounds__(64, 2)
+    k_css_mds_t80(const gd_chrom_dev *ch, int nchrom, const gd_css_planes *pl, const uint32_t *planes,
+                  const int32_t *lo_a_, const int32_t *hi_a_, const int32_t *lo_b_, const double *avals,
+                  const double *bvals, int64_t wtotal, int want_x, int force_literal, double *scores, double *pvals,
+                  double *xbuf, uint8_t *status, unsigned *flags) {
+  constexpr int MP = T80;
+  __shared__ __attribute__((aligned(16))) double s_tail[MP - T80_MAIN][MP];
+  /* the distance build's and the Householder steps' buffers, reused by inverse iteration */
+  __shared__ __attribute__((aligned(16))) union {
+    struct {
+      double row[MP + 2];
+      double v[MP], w[MP];
+      uint64_t mask[2 * MP];
+      double vals[MP];
+    } a;
+    struct {
+      double lu[2][3][MP];
+      double y[2][MP];
+      uint8_t piv[2][MP];
+    } b;
+  } s_u;
+  __shared__ __attribute__((aligned(16))) double s_d[MP + 4];
+  __shared__ __attribute__((aligned(16))) double s_e2[MP + 4];
+  __shared__ double s_e[MP], s_tau[MP];
+  __shared__ double s_x[2 * MP];
+  __shared__ int s_tr[MP];
+  __shared__ double s_lam[2];
+  __shared__ double s_red[4];
+
+  const int tid = threadIdx.x;
+  const int i = tid, tr = tid >> 2, tq = tid & 3, R = T80_MAIN + tr;
+  for (int k = tid; k < MP; k += 64) s_tr[k] = k;
+
+  for (int64_t w = blockIdx.x; w < wtotal; w += wtotal) {
+    CSS_PROF_INIT;
+    const int c = chrom_of(ch, nchrom, w);
+    const gd_chrom_dev &d = ch[c];
+    const int a = d.asize, b = d.bsize, m = a + b;
+    const int64_t wl = w - d.w_base;
+    const int32_t la = lo_a_[w], ha = hi_a_[w], lb = lo_b_[w];
+    const int npos = (ha - la) / a;
+    if (npos <= 0) continue;
+    if ((int64_t)lb + (int64_t)npos * b > d.blen) {
+      if (tid == 0) atomicOr(flags, GD_FLAG_B_BOUNDS);
+      continue;
+    }
+    if (m > MP) {
+      if (tid == 0) atomicOr(flags, GD_FLAG_BAD_SIZE);
+      continue;
+    }
+    const bool row = i < m, trow = R < m;
+    const gd_css_planes P = pl[c];
+    const uint32_t *pa = planes + P.pa, *pb = planes + P.pb;
+    const int64_t ra = la / a, rb = lb / b;
+
+    /* ---- regular window?  (k_css_mds) */
+    bool literal = force_literal || (la % a) != 0 || (lb % b) != 0;
+    if (!literal) {
+      int irr = 0;
+      for (int k = tid; k * 64 < npos; k += 64) {
+        const int nb = min(64, npos - 64 * k);
+        const uint64_t tail = nb == 64 ? ~0ull : ((1ull << nb) - 1);
+        const uint64_t xa = plane_bits64(pa + (int64_t)(2 * a) * P.wa, ra + 64 * k) & tail;
+        const uint64_t xb = plane_bits64(pb + (int64_t)(2 * b) * P.wb, rb + 64 * k) & tail;
+        irr |= (xa | xb) != 0;
+      }
+      literal = __syncthreads_or(irr);
+    }
+
+    /* ---- compare_all: main row i in A, tail row R's columns 4s + tq into s_tail */
+    double A[MP];
+    {
+      int acc[MP], acct[T80_TS];
+#pragma unroll
+      for (int jj = 0; jj < MP; ++jj) acc[jj] = 0;
+#pragma unroll
+      for (int s = 0; s < T80_TS; ++s) acct[s] = 0;
+      if (!literal) {
+        for (int k = 0; k * 64 < npos; ++k) {
+          const int nb = min(64, npos - 64 * k);
+          const uint64_t tail = nb == 64 ? ~0ull : ((1ull << nb) - 1);
+          __syncthreads();
+          for (int r = tid; r < MP; r += 64) {
+            uint64_t Pm = 0, Nm = 0;
+            if (r < m) {
+              const uint32_t *base = r < a ? pa + (int64_t)(2 * r) * P.wa : pb + (int64_t)(2 * (r - a)) * P.wb;
+              const int64_t nw = r < a ? P.wa : P.wb;
+              const int64_t rr = (r < a ? ra : rb) + 64 * k;
+              Pm = plane_bits64(base, rr) & tail;
+              Nm = plane_bits64(base + nw, rr) & tail;
+            }
+            s_u.a.mask[2 * r] = Pm;
+            s_u.a.mask[2 * r + 1] = Nm;
+          }
+          __syncthreads();
+          const uint64_t *mk = s_u.a.mask;
+          const uint64_t Pi = mk[2 * i], Ni = mk[2 * i + 1];
+#pragma unroll
+          for (int jj = 0; jj < MP; ++jj) {
+            acc[jj] += __popcll(Pi & mk[2 * jj + 1]) + __popcll(Ni & mk[2 * jj]);
+            if ((jj & 7) == 7) {
+#pragma unroll
+              for (int u = jj - 7; u <= jj; ++u) CSS_PIN(acc[u]);
+            }
+          }
+          const uint64_t Pt = mk[2 * R], Nt = mk[2 * R + 1];
+#pragma unroll
+          for (int s = 0; s < T80_TS; ++s) {
+            const int j = 4 * s + tq;
+            acct[s] += __popcll(Pt & mk[2 * j + 1]) + __popcll(Nt & mk[2 * j]);
+          }
+        }
+      } else {
+        const double *av = avals + d.a_off + la, *bv = bvals + d.b_off + lb;
+        for (int k = 0; k < npos; ++k) {
+          __syncthreads();
+          for (int r = tid; r < m; r += 64)
+            s_u.a.vals[r] = r < a ? av[(int64_t)k * a + r] : bv[(int64_t)k * b + (r - a)];
+          __syncthreads();
+          const double *sv = s_u.a.vals;
+          int io = i, ro = R, mo = m, ao = a;
+          CSS_OPAQUE_V(io);
+          CSS_OPAQUE_V(ro);
+          CSS_OPAQUE_S(mo);
+          CSS_OPAQUE_S(ao);
+          const double vi = sv[io], vr = sv[ro];
+#pragma unroll
+          for (int jj = 0; jj < MP; ++jj) {
+            /* the diagonal never counts: (int)v * v >= 0 */
+            if (jj < mo) {
+              const double vj = sv[jj];
+              /* the reference casts the row element of the larger index within a
+               * population and the A element across populations (css.c:281-326) */
+              const bool cast_i = ((io < ao) == (jj < ao)) ? (io > jj) : (io < ao);
+              const double prod = cast_i ? x86_int(vi) * vj : x86_int(vj) * vi;
+              acc[jj] += prod == -9.0;
+            }
+          }
+#pragma unroll
+          for (int s = 0; s < T80_TS; ++s) {
+            const int j = 4 * s + tq;
+            if (j < mo) {
+              const double vj = sv[j];
+              const bool cast_r = ((ro < ao) == (j < ao)) ? (ro > j) : (ro < ao);
+              const double prod = cast_r ? x86_int(vr) * vj : x86_int(vj) * vr;
+              acct[s] += prod == -9.0;
+            }
+          }
+        }
+      }
+      int mo = m;
+      CSS_OPAQUE_S(mo);
+#pragma unroll
+      for (int jj = 0; jj < MP; ++jj) A[jj] = (row && jj < mo) ? (double)acc[jj] : 0.0;
+#pragma unroll
+      for (int s = 0; s < T80_TS; ++s) {
+        const int j = 4 * s + tq;
+        s_tail[tr][j] = (trow && j < mo) ? (double)acct[s] : 0.0;
+      }
+    }
+
+    CSS_PROF(0);
+    /* ---- fill_averages (k_css_mds) */
+    {
+      int unval = 0;
+      double sum = 0;
+      int mo = m;
+      CSS_OPAQUE_S(mo);
+#pragma unroll
+      for (int jj = 0; jj < MP; ++jj) {
+        if (row && jj < mo) {
+          if (A[jj] < 0.00001)
+            ++unval;
+          else
+            sum += A[jj];
+        }
+      }
+#pragma unroll
+      for (int s = 0; s < T80_TS; ++s) {
+        const int j = 4 * s + tq;
+        const double t = s_tail[tr][j];
+        if (trow && j < mo) {
+          if (t < 0.00001)
+            ++unval;
+          else
+            sum += t;
+        }
+      }
+      double unv = (double)unval;
+      wave_sum2(unv, sum); /* sums of integers: exact in any order */
+      unval = (int)unv;
+      const int tot = m * m;
+      if (unval > tot / 2) continue; /* discarded window: outputs untouched */
+      const double avg = sum / tot;
+      CSS_OPAQUE_ROW(A);
+#pragma unroll
+      for (int jj = 0; jj < MP; ++jj) A[jj] = fma(avg, 1.0 - fmin(A[jj], 1.0), A[jj]);
+#pragma unroll
+      for (int s = 0; s < T80_TS; ++s) {
+        double *t = &s_tail[tr][4 * s + tq];
+        *t = fma(avg, 1.0 - fmin(*t, 1.0), *t);
+      }
+    }
+
+    /* ---- B = -1/2 Z (D o D) Z by double centering */
+    double zero_tol;
+    {
+      double rs = 0, rst = 0;
+      int mo = m;
+      CSS_OPAQUE_S(mo);
+#pragma unroll
+      for (int jj = 0; jj < MP; ++jj) {
+        A[jj] = (row && jj < mo) ? A[jj] * A[jj] : 0.0;
+        rs += A[jj];
+      }
+#pragma unroll
+      for (int s = 0; s < T80_TS; ++s) {
+        const int j = 4 * s + tq;
+        double *t = &s_tail[tr][j];
+        const double sq = (trow && j < mo) ? *t * *t : 0.0;
+        *t = sq;
+        rst += sq;
+      }
+      rst = quad_sum(rst);
+      const double ri = row ? rs / m : 0.0, rt = trow ? rst / m : 0.0;
+      __syncthreads();
+      s_u.a.v[i] = ri;
+      if (tq == 0) s_u.a.v[R] = rt;
+      const double g = block_sum<1>(ri + (tq == 0 ? rt : 0.0), s_red) / m;
+      __syncthreads();
+      const double *sv = s_u.a.v;
+      CSS_OPAQUE_S(mo);
+#pragma unroll
+      for (int jj = 0; jj < MP; ++jj) {
+        A[jj] = (row && jj < mo) ? -0.5 * ((A[jj] - (ri + sv[jj])) + g) : 0.0;
+        if ((jj & 7) == 7) {
+#pragma unroll
+          for (int u = jj - 7; u <= jj; ++u) CSS_PIN(A[u]);
+        }
+      }
+      double f2 = 0;
+#pragma unroll
+      for (int jj = 0; jj < MP; ++jj) f2 = fma(A[jj], A[jj], f2);
+#pragma unroll
+      for (int s = 0; s < T80_TS; ++s) {
+        const int j = 4 * s + tq;
+        double *t = &s_tail[tr][j];
+        const double cv = (trow && j < mo) ? -0.5 * ((*t - (rt + sv[j])) + g) : 0.0;
+        *t = cv;
+        f2 = fma(cv, cv, f2);
+      }
+      /* eigenvalues within rounding of 0 count as 0 (oracle/css_oracle.c, cmds) */
+      zero_tol = 64.0 * m * DBL_EPSILON * sqrt(block_sum<1>(f2, s_red));
+    }
+
+    CSS_PROF(1);
+    /* ---- Householder tridiagonalisation (LAPACK dsytd2, lower; k_css_mds) */
+#ifndef GD_CSS_SKIP_TRIDIAG
+    T80Steps<0>::run(A, m, s_u.a.row, s_u.a.v, s_u.a.w, s_d, s_e, s_tau, s_tail);
+#endif
+    __syncthreads();
+
+    CSS_PROF(2);
+    /* ---- the two largest eigenvalues of T (k_css_mds) */
+    double glo, ghi;
+    {
+      double lo = DBL_MAX, hi = -DBL_MAX;
+      if (row) {
+        const double r = (i > 0 ? fabs(s_e[i - 1]) : 0.0) + (i < m - 1 ? fabs(s_e[i]) : 0.0);
+        lo = s_d[i] - r;
+        hi = s_d[i] + r;
+      }
+      if (tq == 0 && trow) {
+        const double r = fabs(s_e[R - 1]) + (R < m - 1 ? fabs(s_e[R]) : 0.0);
+        lo = fmin(lo, s_d[R] - r);
+        hi = fmax(hi, s_d[R] + r);
+      }
+      for (int k = tid; k < MP + 4; k += 64) s_e2[k] = (k >= 1 && k < m) ? s_e[k - 1] * s_e[k - 1] : 0.0;
+      glo = block_reduce<1, OpMin>(lo, s_red);
+      ghi = block_reduce<1, OpMax>(hi, s_red);
+      const double pad = 2.0 * DBL_EPSILON * fmax(fabs(glo), fabs(ghi)) * m + DBL_MIN;
+      glo -= pad;
+      ghi += pad;
+      for (int k = tid; k < MP + 4; k += 64)
+        if (k >= m) s_d[k] = 2.0 * fabs(ghi) + 2.0 * fabs(glo) + 1.0;
+    }
+    const double bis_tol = CSS_BISECT_TOL * fmax(fabs(glo), fabs(ghi)) + DBL_MIN;
+    __syncthreads();
+    bisect_top2(m, glo, ghi, bis_tol, s_d, s_e2, s_lam, tid);
+    __syncthreads();
+
+    CSS_PROF(3);
+    /* ---- eigenvectors of T: two steps of inverse iteration (k_css_mds) */
+    if (tid < 2) invit_factor<MP>(m, tid, s_d, s_e, s_lam, s_u.b.lu, s_x, s_u.b.piv, s_u.b.y);
+    __syncthreads();
+    {
+      const double tiny = DBL_EPSILON * fmax(fmax(fabs(glo), fabs(ghi)), DBL_MIN);
+      for (int k = tid; k < m; k += 64) {
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const double u0 = s_u.b.lu[e][0][k];
+          s_u.b.lu[e][0][k] = fast_rcp(u0 == 0.0 ? tiny : u0);
+        }
+      }
+    }
+    double y1 = 0.0, y2 = 0.0, y1t = 0.0, y2t = 0.0;
+#ifdef GD_CSS_SKIP_INVIT
+    for (int itn = 0; itn < 0; ++itn) {
+#else
+    for (int itn = 0; itn < 2; ++itn) {
+#endif
+      __syncthreads();
+      if (tid < 2) invit_solve<MP>(m, tid, s_u.b.lu, s_x, s_u.b.piv, s_u.b.y);
+      __syncthreads();
+      y1 = row ? s_u.b.y[0][i] : 0.0;
+      y2 = row ? s_u.b.y[1][i] : 0.0;
+      y1t = trow ? s_u.b.y[0][R] : 0.0;
+      y2t = trow ? s_u.b.y[1][R] : 0.0;
+      double n1 = y1 * y1 + (tq == 0 ? y1t * y1t : 0.0), n2 = y2 * y2 + (tq == 0 ? y2t * y2t : 0.0);
+      wave_sum2(n1, n2);
+      const double r1 = 1.0 / sqrt(n1), r2 = 1.0 / sqrt(n2);
+      y1 *= r1;
+      y2 *= r2;
+      y1t *= r1;
+      y2t *= r2;
+      __syncthreads();
+      if (itn == 0) {
+        if (row) {
+          s_u.b.y[0][i] = y1;
+          s_u.b.y[1][i] = y2;
+        }
+        if (tq == 0 && trow) {
+          s_u.b.y[0][R] = y1t;
+          s_u.b.y[1][R] = y2t;
+        }
+      }
+    }
+    /* orthogonalise the second vector against the first (close eigenvalues) */
+    {
+      double dt = y1 * y2 + (tq == 0 ? y1t * y2t : 0.0), zero = 0.0;
+      wave_sum2(dt, zero);
+      y2 = fma(-dt, y1, y2);
+      y2t = fma(-dt, y1t, y2t);
+      double n2 = y2 * y2 + (tq == 0 ? y2t * y2t : 0.0);
+      zero = 0.0;
+      wave_sum2(n2, zero);
+      const double r2 = 1.0 / sqrt(n2);
+      y2 *= r2;
+      y2t *= r2;
+    }
+    /* eigenvalues = Rayleigh quotients y^T T y of the unit vectors (k_css_mds) */
+    {
+      double(*sy)[MP] = s_u.b.y;
+      __syncthreads();
+      if (row) {
+        sy[0][i] = y1;
+        sy[1][i] = y2;
+      }
+      if (tq == 0 && trow) {
+        sy[0][R] = y1t;
+        sy[1][R] = y2t;
+      }
+      __syncthreads();
+      double t1 = 0.0, t2 = 0.0;
+      if (row) {
+        const double el = i > 0 ? s_e[i - 1] : 0.0, er = i + 1 < m ? s_e[i] : 0.0;
+        const int il = i > 0 ? i - 1 : 0, ir = i + 1 < m ? i + 1 : i;
+        t1 = y1 * (s_d[i] * y1 + el * sy[0][il] + er * sy[0][ir]);
+        t2 = y2 * (s_d[i] * y2 + el * sy[1][il] + er * sy[1][ir]);
+      }
+      if (tq == 0 && trow) {
+        const double el = s_e[R - 1], er = R + 1 < m ? s_e[R] : 0.0;
+        const int il = R - 1, ir = R + 1 < m ? R + 1 : R;
+        t1 += y1t * (s_d[R] * y1t + el * sy[0][il] + er * sy[0][ir]);
+        t2 += y2t * (s_d[R] * y2t + el * sy[1][il] + er * sy[1][ir]);
+      }
+      wave_sum2(t1, t2);
+      if (tid == 0) {
+        s_lam[0] = fabs(t1) <= zero_tol ? 0.0 : t1;
+        s_lam[1] = fabs(t2) <= zero_tol ? 0.0 : t2;
+      }
+      __syncthreads();
+    }
+
+    CSS_PROF(4);
+    /* ---- back-transformation y <- H_0 H_1 ... H_{m-3} y; v_k sits in column k */
+#ifndef GD_CSS_SKIP_BACK
+#pragma unroll
+    for (int k = MP - 3; k >= 0; --k) {
+      if (k <= m - 3) {
+        const double vk = row ? A[k] : 0.0;
+        const double vkt = trow ? s_tail[tr][k] : 0.0;
+        const double t = s_tau[k];
+        double d1 = vk * y1 + (tq == 0 ? vkt * y1t : 0.0), d2 = vk * y2 + (tq == 0 ? vkt * y2t : 0.0);
+        wave_sum2(d1, d2);
+        y1 = fma(-(t * d1), vk, y1);
+        y2 = fma(-(t * d2), vk, y2);
+        y1t = fma(-(t * d1), vkt, y1t);
+        y2t = fma(-(t * d2), vkt, y2t);
+        asm volatile("" ::: "memory"); /* one s_tau load in flight, not MP */
+      }
+    }
+#endif
+
+    CSS_PROF(5);
+    /* ---- X = Q sqrt(L) (css.c:545-556), then calc_dist + css on identity groups */
+    {
+      const double L1 = sqrt(s_lam[0]), L2 = sqrt(s_lam[1]);
+      __syncthreads();
+      if (row) {
+        s_x[2 * i] = y1 * L1 + y2 * 0.0;
+        s_x[2 * i + 1] = y1 * 0.0 + y2 * L2;
+      }
+      if (tq == 0 && trow) {
+        s_x[2 * R] = y1t * L1 + y2t * 0.0;
+        s_x[2 * R + 1] = y1t * 0.0 + y2t * L2;
+      }
+      __syncthreads();
+    }
+    const double score = css_score<1>(s_tr, a, b, [&](int p, int q) { return xdist(s_x, p, q); }, s_red);
+    CSS_PROF(6);
+    if (score == -1.0) continue; /* the reference's "discarded" marker (css.c:127) */
+    if (tid == 0) {
+      scores[d.w_out + wl] = score;
+      if (!want_x) pvals[d.w_out + wl] = 1.0; /* runs == 0: p = (0 + 1) / (0 + 1) */
+    }
+    if (want_x) {
+      for (int e = tid; e < 2 * MP; e += 64) xbuf[w * 2 * MP + e] = (e < 2 * m) ? s_x[e] : 0.0;
+      if (tid == 0) status[w] = 1;
+    }
+  }
+}
+
 /* the other stages of a scan (gd_css_perm.hip, gd_css_smacof.hip, gd_packed.hip) */
 int gd_packed_css_planes_launch(const gd_chrom_dev *d_ch, int nchrom, const gd_css_planes *d_pl,
                                 const int64_t *word_off, const uint64_t *acodes, const uint64_t *bcodes,
@@ -1175,6 +1803,15 @@ int gd_css_tier(int m) {
   for (int t : tiers)
     if (m <= t) return t;
   return 0;
+}
+
+static int launch_t80(const gd_chrom_dev *d_ch, int nchrom, const gd_css_planes *d_pl, const uint32_t *planes,
+                      const int32_t *lo_a, const int32_t *hi_a, const int32_t *lo_b, const double *avals,
+                      const double *bvals, int64_t wtotal, int want_x, int force_literal, double *scores, double *p,
+                      double *xbuf, uint8_t *status, unsigned *flags, hipStream_t s) {
+  hipLaunchKernelGGL(k_css_mds_t80, dim3((unsigned)wtotal), dim3(64), 0, s, d_ch, nchrom, d_pl, planes, lo_a, hi_a,
+                     lo_b, avals, bvals, wtotal, want_x, force_literal, scores, p, xbuf, status, flags);
+  return hipGetLastError() == hipSuccess ? GD_OK : GD_ERR_HIP;
 }
 
 template <int MP, int G>
@@ -1246,7 +1883,14 @@ int gd_css_launch(int mp, int drosophila, int mds, const gd_chrom_dev *d_ch, int
         CSS_TIER(24, 1)
         CSS_TIER(40, 1)
         CSS_TIER(64, 1)
+#if CSS_T80
+        case 80:
+          st = launch_t80(d_ch, nchrom, d_pl, planes, lo_a, hi_a, lo_b, avals, bvals, wtotal, want_x1, force_literal,
+                          scores, p, xbuf, status, flags, s);
+          break;
+#else
         CSS_TIER(80, CSS_G80)
+#endif
         CSS_TIER(96, 2)
         CSS_TIER(128, 2)
         default:
