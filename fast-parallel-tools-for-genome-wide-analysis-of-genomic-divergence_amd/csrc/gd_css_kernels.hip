@@ -56,6 +56,9 @@ __device__ unsigned long long g_css_prof[8];
 /* waves per SIMD the register allocator must reach for k_css_mds<MP> (measured per
  * tier: MP = 24 fits 5 waves without spills, MP = 40 runs best at 4 with a few cold
  * spills) */
+#ifndef CSS_STATIC_G1_MAX
+#define CSS_STATIC_G1_MAX 64 /* largest one-lane-per-row tier with compile-time-K steps (64: 29.7 -> 18.4 ms per 200k 32+32 windows) */
+#endif
 #ifndef CSS_STATIC_G2_MAX
 #define CSS_STATIC_G2_MAX 80 /* largest G = 2 tier with compile-time-K steps */
 #endif
@@ -924,7 +927,7 @@ __global__ void __launch_bounds__((CssShape<MP, G>::NT), CSS_MDS_WAVES(MP, G))
      * of each row holds that row's element of the reflector v_k.  Columns are
      * handled in blocks of 8; a block dead in every column part (v, w and x are 0
      * left of k) is skipped by a uniform branch. */
-    if constexpr (G == 1 && MP <= 40) {
+    if constexpr (G == 1 && MP <= CSS_STATIC_G1_MAX) {
 #ifndef GD_CSS_SKIP_TRIDIAG
       HhStatic<MP, 0>::run(A, m, s_row, s_v, s_w, s_d, s_e, s_tau);
 #endif
