@@ -1196,6 +1196,10 @@ __global__ void __launch_bounds__((CssShape<MP, G>::NT), CSS_MDS_WAVES(MP, G))
 /* ------------------------------------------------------------------------ */
 namespace {
 constexpr int T80 = 80, T80_MAIN = 64, T80_TS = 20; /* order, VGPR rows, tail columns per lane */
+/* tail row stride in doubles: 2 * 84 = 40 (mod 64) dwords, so the 8 tail rows of a
+ * 32-lane group start 8 banks apart and a quad's 4 columns fill its 8 banks (a stride of
+ * 80 doubles put 4 rows on the same banks: 4-way conflicts on every tail access) */
+constexpr int T80_TSTRIDE = 84;
 
 /* sum over the 4 lanes of a quad (every lane gets the same bits) */
 __device__ __forceinline__ double quad_sum(double x) {
@@ -1206,7 +1210,7 @@ __device__ __forceinline__ double quad_sum(double x) {
 /* One Householder step (hh_step_static) over the main rows and the LDS tail. */
 template <int K>
 __device__ __forceinline__ void t80_step(double (&A)[T80], int m, double *s_row, double *s_v, double *s_w,
-                                         double *s_d, double *s_e, double *s_tau, double (*s_tail)[T80]) {
+                                         double *s_d, double *s_e, double *s_tau, double (*s_tail)[T80_TSTRIDE]) {
   constexpr int MP = T80;
   const int i = css_lane_now(), tr = i >> 2, tq = i & 3, R = T80_MAIN + tr;
   const bool row = i < m, trow = R < m;
@@ -1338,7 +1342,7 @@ __device__ __forceinline__ void t80_step(double (&A)[T80], int m, double *s_row,
 template <int K>
 struct T80Steps {
   static __device__ __forceinline__ void run(double (&A)[T80], int m, double *s_row, double *s_v, double *s_w,
-                                             double *s_d, double *s_e, double *s_tau, double (*s_tail)[T80]) {
+                                             double *s_d, double *s_e, double *s_tau, double (*s_tail)[T80_TSTRIDE]) {
     if ((K & 7) == 0 && K >= m) return; /* exits only at block boundaries (hh_step_static) */
     t80_step<K>(A, m, s_row, s_v, s_w, s_d, s_e, s_tau, s_tail);
     T80Steps<K + 1>::run(A, m, s_row, s_v, s_w, s_d, s_e, s_tau, s_tail);
@@ -1347,7 +1351,7 @@ struct T80Steps {
 template <>
 struct T80Steps<T80> {
   static __device__ __forceinline__ void run(double (&)[T80], int, double *, double *, double *, double *, double *,
-                                             double *, double (*)[T80]) {}
+                                             double *, double (*)[T80_TSTRIDE]) {}
 };
 }  // namespace
 
@@ -1357,10 +1361,11 @@ __global__ void __launch_bounds__(64, 2)
                   const double *bvals, int64_t wtotal, int want_x, int force_literal, double *scores, double *pvals,
                   double *xbuf, uint8_t *status, unsigned *flags) {
   constexpr int MP = T80;
-  __shared__ __attribute__((aligned(16))) double s_tail[MP - T80_MAIN][MP];
+  __shared__ __attribute__((aligned(16))) double s_tail[MP - T80_MAIN][T80_TSTRIDE];
   /* the distance build's and the Householder steps' buffers, reused by inverse iteration */
   __shared__ __attribute__((aligned(16))) union {
     struct {
+      double e2[MP + 4]; /* bisection only (after the Householder steps) */
       double row[MP + 2];
       double v[MP], w[MP];
       uint64_t mask[2 * MP];
@@ -1373,7 +1378,7 @@ __global__ void __launch_bounds__(64, 2)
     } b;
   } s_u;
   __shared__ __attribute__((aligned(16))) double s_d[MP + 4];
-  __shared__ __attribute__((aligned(16))) double s_e2[MP + 4];
+  double *s_e2 = s_u.a.e2;
   __shared__ double s_e[MP], s_tau[MP];
   __shared__ double s_x[2 * MP];
   __shared__ int s_tr[MP];
