@@ -28,7 +28,9 @@ def _cmp_scores(s, s_ref, rel=1e-9):
 
 
 @pytest.mark.parametrize("asize,bsize,nsnp", [(10, 10, 60_000), (20, 20, 30_000), (7, 13, 30_000), (40, 40, 4_000),
-                                              (1, 1, 20_000), (33, 31, 6_000), (45, 45, 3_000)])
+                                              (1, 1, 20_000), (33, 31, 6_000), (45, 45, 3_000),
+                                              # the one-wave 80 tier: 1, 8 and 9 tail rows (m = 65, 72, 73)
+                                              (33, 32, 3_000), (30, 42, 3_000), (43, 30, 3_000)])
 def test_scores_match_oracle(oracle, asize, bsize, nsnp):
     from gdscan import css
     av, bv, ap, bp, regend = _synth(3, nsnp, asize, bsize)
