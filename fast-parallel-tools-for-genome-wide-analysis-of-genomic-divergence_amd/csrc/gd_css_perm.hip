@@ -355,7 +355,9 @@ __global__ void __launch_bounds__(PermShape<MP>::NT) PERM_WPE
           int li = lane;
           PERM_OPAQUE(li);
           const bool r0 = li < m, r1 = MP > 64 && li + 64 < m;
-          uint32_t car0 = s_car[li], car1 = MP > 64 ? s_car[li + 64] : 0u;
+          /* above 64 individuals lane i carries F(i) and F(i + 64) as the low two bytes of
+           * one word, so one ds_bpermute per row fetches whichever of the two is wanted */
+          uint32_t car = (uint32_t)s_car[li] | (MP > 64 ? (uint32_t)s_car[li + 64] << 8 : 0u);
 #pragma unroll
           for (int q = 0; q < 16; ++q) {
             pf0[q] = r0 ? *reinterpret_cast<const uint32_t *>(my_sig + li * 64 + 4 * q) : 0u;
@@ -364,23 +366,22 @@ __global__ void __launch_bounds__(PermShape<MP>::NT) PERM_WPE
 #pragma unroll
           for (int t = 0; t < 64; ++t) {
             const uint32_t s0 = (pf0[t >> 2] >> (8 * (t & 3))) & 0xFFu;
-            uint32_t n0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(s0 << 2), (int)car0);
-            uint32_t n1 = 0;
+            uint32_t n0, n1 = 0;
             if constexpr (MP > 64) {
               const uint32_t s1 = (pf1[t >> 2] >> (8 * (t & 3))) & 0xFFu;
-              const uint32_t g0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((s0 & 63u) << 2), (int)car1);
-              n0 = s0 < 64 ? n0 : g0;
-              const uint32_t h0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((s1 & 63u) << 2), (int)car0);
-              const uint32_t h1 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((s1 & 63u) << 2), (int)car1);
-              n1 = s1 < 64 ? h0 : h1;
+              const uint32_t a0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((s0 & 63u) << 2), (int)car);
+              const uint32_t a1 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((s1 & 63u) << 2), (int)car);
+              n0 = (s0 < 64 ? a0 : a0 >> 8) & 0xFFu;
+              n1 = (s1 < 64 ? a1 : a1 >> 8) & 0xFFu;
               if (r1) my_sig[(li + 64) * 64 + t] = (uint8_t)n1;
+            } else {
+              n0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(s0 << 2), (int)car);
             }
             if (r0) my_sig[li * 64 + t] = (uint8_t)n0;
-            car0 = n0;
-            car1 = n1;
+            car = n0 | (n1 << 8);
           }
-          if (r0) s_car[li] = (uint8_t)car0;
-          if (r1) s_car[li + 64] = (uint8_t)car1;
+          if (r0) s_car[li] = (uint8_t)car;
+          if (r1) s_car[li + 64] = (uint8_t)(car >> 8);
         }
         __syncthreads();
       }
