@@ -26,6 +26,7 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <cstdlib>
 
 #include "../../include/gdscan.h"
 #include "gd_common.h"
@@ -74,7 +75,12 @@ __device__ __forceinline__ double perm_xdist(const double *X, int i, int j) {
   return sqrt(dx * dx + dy * dy);
 }
 
-/* waves per workgroup: the LDS (S triangle + per-wave byte matrices) sets it */
+/* Row stride of the byte matrices: row k holds byte k of every lane's column.  68
+ * bytes (17 dwords, odd) put the 64 rows a composition step writes, one per lane,
+ * on distinct LDS banks; 64 bytes put them all on two. */
+#define PERM_ROW 68
+
+/* waves per workgroup and the LDS carve-up */
 template <int MP>
 struct PermShape {
   static constexpr int TRI = MP * (MP + 1) / 2 + 1; /* packed triangle + padding row + zero */
@@ -84,12 +90,22 @@ struct PermShape {
 #endif
   static constexpr int NWV = MP <= 64 ? 4 : PERM_NWV_LARGE;
   static constexpr int NT = 64 * NWV;
+  static constexpr int SIG = MP * PERM_ROW; /* one wave's byte matrix */
+  static constexpr int MEM = HALF * 64;     /* one wave's member lists (byte k of lane l at k*64 + l) */
+  /* region U: the FP64 triangle while a window is set up, then the FP32 triangle, the
+   * byte matrices and the member lists */
+  static constexpr int OFF_SIG = (TRI * 4 + 15) / 16 * 16;
+  static constexpr int OFF_MEM = OFF_SIG + NWV * SIG;
+  static constexpr int UBYTES = OFF_MEM + NWV * MEM > TRI * 8 ? OFF_MEM + NWV * MEM : TRI * 8;
+  static_assert(NWV * MEM >= (NT + 1) * 8, "the serial-stream start states alias the member lists");
 };
 
 /* packed lower triangle with one zero row appended: pair (x, y), x != y, at
  * T(max) + min, T(h) = h(h-1)/2; index MP is a padding individual with S = 0, and
- * the pair (MP, MP) lands on the extra zero entry at the end */
+ * the pair (MP, MP) lands on the extra zero entry at the end.  Byte offsets of T(x)
+ * for the FP64 (tri8) and FP32 (tri4) copies. */
 __device__ __forceinline__ uint32_t tri8(uint32_t x) { return (x * (x - 1u) >> 1) << 3; }
+__device__ __forceinline__ uint32_t tri4(uint32_t x) { return (x * (x - 1u) >> 1) << 2; }
 
 /* S(x, y) for two individuals given their tri8 forms */
 __device__ __forceinline__ double s_pair(const double *S, uint32_t x, uint32_t tx, uint32_t y, uint32_t ty) {
@@ -97,44 +113,145 @@ __device__ __forceinline__ double s_pair(const double *S, uint32_t x, uint32_t t
   return *reinterpret_cast<const double *>(reinterpret_cast<const char *>(S) + off);
 }
 
-/* css() of the track array in column `lane` of sig (byte k at sig[k*64 + lane]).
- * The consecutive within-group pairs (css.c:627-642) are summed first, in track
- * order; the smaller group G is collected as a bit set on the way and then written
- * back over the head of the column in ascending order (the column is dead after
- * the score).  With the members ascending, pair (u < v) sits at T(x_v) + x_u with no
- * compare, and the between-group term becomes a function of the SET G alone, so
- * every permutation that keeps the groups' sets gets the observed value bit for bit.
- * Pairs are visited in 8x8 blocks of members (runtime block loops, unrolled blocks),
- * which bounds both the code and the loads in flight. */
+/* css() of one track array in FP64.  track(k): entry k of the track array; member(k):
+ * member k of the smaller group G in ascending order, the padding individual MP for
+ * k >= g; sxy(x, y), x < y: S(x, y) (0 when y is the padding individual).  The
+ * consecutive within-group pairs (css.c:627-642) are summed in track order; the
+ * between-group sum over G is sum_{x in G} R_x - 2 sum_{x<y in G} S_xy with the members
+ * ascending, visited in 8x8 blocks, so it is a function of the SET G alone: every
+ * permutation that keeps the groups' sets gets the observed value bit for bit. */
+template <int MP, bool UNROLL, class TRK, class MEMB, class SXY>
+__device__ __forceinline__ double score_exact(TRK track, MEMB member, SXY sxy, const double *R, int a, int b,
+                                              double inva, double invb) {
+  constexpr int NB = (PermShape<MP>::HALF + 7) / 8;
+  const int m = a + b;
+  double wa = 0.0, wb = 0.0;
+  uint32_t prev = track(0);
+#pragma unroll 4
+  for (int k = 1; k < m; ++k) {
+    const uint32_t cur = track(k);
+    const double e = sxy(min(prev, cur), max(prev, cur));
+    if (k < a) wa += e;
+    if (k > a) wb += e;
+    prev = cur;
+  }
+  double sr = 0.0, q0 = 0.0, q1 = 0.0, q2 = 0.0, q3 = 0.0;
+  if constexpr (UNROLL) {
+    /* the observed score (once per window, S from the triangle): many loads in flight */
+#pragma unroll 1
+    for (int K = 0; K < NB; ++K) {
+      uint32_t xk[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        xk[u] = member(8 * K + u);
+        sr += R[xk[u]];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+#pragma unroll
+        for (int v = u + 1; v < 8; ++v) {
+          const double e = sxy(xk[u], xk[v]);
+          if ((u + v) & 1)
+            q0 += e;
+          else
+            q1 += e;
+        }
+        asm volatile("" ::: "memory");
+      }
+#pragma unroll 1
+      for (int L = K + 1; L < NB; ++L) {
+        uint32_t xl[8];
+#pragma unroll
+        for (int v = 0; v < 8; ++v) xl[v] = member(8 * L + v);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+#pragma unroll
+          for (int v = 0; v < 8; ++v) {
+            const double e = sxy(xk[u], xl[v]);
+            if (v & 1)
+              q3 += e;
+            else
+              q2 += e;
+          }
+          asm volatile("" ::: "memory");
+        }
+      }
+    }
+  } else {
+    /* rolled (the rare ambiguous lanes, S from the coordinates); the additions reach
+     * each accumulator in the same order */
+#pragma unroll 1
+    for (int K = 0; K < NB; ++K) {
+#pragma unroll 1
+      for (int u = 0; u < 8; ++u) sr += R[member(8 * K + u)];
+#pragma unroll 1
+      for (int u = 0; u < 8; ++u) {
+        const uint32_t xu = member(8 * K + u);
+#pragma unroll 1
+        for (int v = u + 1; v < 8; ++v) {
+          const double e = sxy(xu, member(8 * K + v));
+          if ((u + v) & 1)
+            q0 += e;
+          else
+            q1 += e;
+        }
+      }
+#pragma unroll 1
+      for (int L = K + 1; L < NB; ++L)
+#pragma unroll 1
+        for (int u = 0; u < 8; ++u) {
+          const uint32_t xu = member(8 * K + u);
+#pragma unroll 1
+          for (int v = 0; v < 8; ++v) {
+            const double e = sxy(xu, member(8 * L + v));
+            if (v & 1)
+              q3 += e;
+            else
+              q2 += e;
+          }
+        }
+    }
+  }
+  const double bet = sr - 2.0 * ((q0 + q1) + (q2 + q3));
+  return bet / (double)(a * b) - (double)(a + b) * (wa * inva + wb * invb);
+}
+
+/* The same score from the FP32 copy of S, with a bound on its distance to the FP64
+ * value score_exact returns: est, err with |score_exact - est| <= err.  Every S
+ * entry is >= 0, so a sum of n FP32-rounded terms is within (n + 2) 2^-24 of its
+ * computed value (representation + recursive summation), plus 2^-125 per term for
+ * flushed subnormals; the FP64 sums and the final arithmetic of both versions add
+ * < 1e-11 of the magnitudes involved.  Reads the track from column `col` (byte k
+ * at col[k*PERM_ROW]) and writes G's members ascending to `mcol` (the track stays intact
+ * for score_exact).  sr, the row-sum term, is summed exactly as score_exact sums it. */
 template <int MP>
-__device__ __forceinline__ double perm_score(const double *S, const double *R, uint8_t *sig, int lane, int a, int b,
-                                             double inva, double invb) {
+__device__ __forceinline__ void score_f32(const float *S32, const double *R, const uint8_t *col, uint8_t *mcol, int a,
+                                          int b, double inva, double invb, double &est, double &err) {
   constexpr int NB = (PermShape<MP>::HALF + 7) / 8;
   const int m = a + b;
   const int g = a <= b ? a : b, off = a <= b ? 0 : a;
-  PERM_OPAQUE(lane);
-  uint8_t *col = sig + lane;
-  const char *Sb = reinterpret_cast<const char *>(S);
+  const char *Sb = reinterpret_cast<const char *>(S32);
+  auto s_at = [&](uint32_t off4) { return *reinterpret_cast<const float *>(Sb + off4); };
   /* consecutive pairs inside each group, and G as a bit set */
-  double wa = 0.0, wb = 0.0;
+  float wa = 0.f, wb = 0.f;
   uint64_t lo = 0, hi = 0;
   auto add_member = [&](uint32_t x) {
     lo |= x < 64 ? 1ull << (x & 63u) : 0ull;
     if constexpr (MP > 64) hi |= x >= 64 ? 1ull << (x & 63u) : 0ull;
   };
-  uint32_t prev = col[0], tprev = tri8(prev);
+  uint32_t prev = col[0], tprev = tri4(prev);
   if (off == 0 && g > 0) add_member(prev);
 #pragma unroll 4
   for (int k = 1; k < m; ++k) {
-    const uint32_t cur = col[k * 64], tcur = tri8(cur);
-    const double e = s_pair(S, prev, tprev, cur, tcur);
+    const uint32_t cur = col[k * PERM_ROW], tcur = tri4(cur);
+    const float e = s_at(prev > cur ? tprev + (cur << 2) : tcur + (prev << 2));
     if (k < a) wa += e;
     if (k > a) wb += e;
     if (k >= off && k < off + g) add_member(cur);
     prev = cur;
     tprev = tcur;
   }
-  /* the members, ascending, over bytes 0 .. g-1 of the column */
+  /* the members, ascending */
 #pragma unroll 4
   for (int k = 0; k < g; ++k) {
     uint32_t x;
@@ -145,55 +262,60 @@ __device__ __forceinline__ double perm_score(const double *S, const double *R, u
       x = 64u + (uint32_t)__builtin_ctzll(hi);
       hi &= hi - 1;
     }
-    col[k * 64] = (uint8_t)x;
+    mcol[k * 64] = (uint8_t)x;
   }
-  /* member k of G, padded with the zero individual MP (the largest index) */
-  auto member = [&](int k) -> uint32_t { return k < g ? (uint32_t)col[k * 64] : (uint32_t)MP; };
-  auto s_at = [&](uint32_t off8) { return *reinterpret_cast<const double *>(Sb + off8); };
-  double sr = 0.0, q0 = 0.0, q1 = 0.0, q2 = 0.0, q3 = 0.0;
+  auto member = [&](int k) -> uint32_t { return k < g ? (uint32_t)mcol[k * 64] : (uint32_t)MP; };
+  /* gathers in pairs, summed with packed FP32 adds (v_pk_add_f32) */
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  double sr = 0.0;
+  f2 qa = {0.f, 0.f}, qb = {0.f, 0.f};
 #pragma unroll 1
   for (int K = 0; K < NB; ++K) {
-    uint32_t xk8[8], tk[8];
+    uint32_t xk4[8], tk[8];
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const uint32_t x = member(8 * K + u);
       sr += R[x];
-      xk8[u] = x << 3;
-      tk[u] = tri8(x);
+      xk4[u] = x << 2;
+      tk[u] = tri4(x);
     }
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
+    for (int u = 0; u < 7; ++u) {
 #pragma unroll
-      for (int v = u + 1; v < 8; ++v) {
-        const double e = s_at(tk[v] + xk8[u]); /* x_u < x_v */
-        if ((u + v) & 1)
-          q0 += e;
-        else
-          q1 += e;
+      for (int v = u + 1; v < 8; v += 2) {
+        f2 e;
+        e.x = s_at(tk[v] + xk4[u]); /* x_u < x_v */
+        e.y = v + 1 < 8 ? s_at(tk[v + 1] + xk4[u]) : 0.f;
+        qa += e;
       }
-      asm volatile("" ::: "memory"); /* a bounded number of gathers in flight */
+      if (u & 1) asm volatile("" ::: "memory"); /* a bounded number of gathers in flight */
     }
 #pragma unroll 1
     for (int L = K + 1; L < NB; ++L) {
       uint32_t tl[8];
 #pragma unroll
-      for (int v = 0; v < 8; ++v) tl[v] = tri8(member(8 * L + v));
+      for (int v = 0; v < 8; ++v) tl[v] = tri4(member(8 * L + v));
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
 #pragma unroll
-        for (int v = 0; v < 8; ++v) {
-          const double e = s_at(tl[v] + xk8[u]); /* every member of block K < every member of block L */
-          if (v & 1)
-            q3 += e;
-          else
-            q2 += e;
+        for (int v = 0; v < 8; v += 2) {
+          f2 e;
+          e.x = s_at(tl[v] + xk4[u]); /* every member of block K < every member of block L */
+          e.y = s_at(tl[v + 1] + xk4[u]);
+          qb += e;
         }
-        asm volatile("" ::: "memory");
+        if (u & 1) asm volatile("" ::: "memory");
       }
     }
   }
-  const double bet = sr - 2.0 * ((q0 + q1) + (q2 + q3));
-  return bet / (double)(a * b) - (double)(a + b) * (wa * inva + wb * invb);
+  const double q = (double)((qa.x + qa.y) + (qb.x + qb.y)), dwa = (double)wa, dwb = (double)wb;
+  const double ab = (double)(a * b), apb = (double)(a + b);
+  est = (sr - 2.0 * q) / ab - apb * (dwa * inva + dwb * invb);
+  constexpr double U = 0x1p-24 * 1.001, SUB = 0x1p-125;
+  const double nq = (double)(g * (g - 1) / 2 + 4);
+  const double eq = nq * (U * q + SUB), ewa = (a + 2) * (U * dwa + SUB), ewb = (b + 2) * (U * dwb + SUB);
+  const double mag = (fabs(sr) + 2.0 * q) / ab + apb * (dwa * inva + dwb * invb);
+  err = 2.0 * eq / ab + apb * (ewa * inva + ewb * invb) + 1e-11 * mag;
 }
 
 /* every lane's column of one wave's byte matrix := identity (rows k < m; row k is
@@ -201,42 +323,59 @@ __device__ __forceinline__ double perm_score(const double *S, const double *R, u
 __device__ __forceinline__ void sig_identity(uint8_t *sig, int m, int lane) {
   PERM_OPAQUE(lane);
   for (int q = lane; q < m * 16; q += 64)
-    *reinterpret_cast<uint32_t *>(sig + (q >> 4) * 64 + (q & 15) * 4) = (uint32_t)(q >> 4) * 0x01010101u;
+    *reinterpret_cast<uint32_t *>(sig + (q >> 4) * PERM_ROW + (q & 15) * 4) = (uint32_t)(q >> 4) * 0x01010101u;
+}
+
+/* random_int_nrand48(n) constants for 2 <= n <= 128 from the magic number alone
+ * (gd_randint_make): shift = ceil(log2 n) - 1, and the rejection limit
+ * RAND_MAX - 2^31 mod n from (2^31 - 1) mod n.  n is wave-uniform, so this is
+ * scalar work; the magic comes from a 4-byte-per-n LDS table. */
+__device__ __forceinline__ gd_randint perm_rd(uint32_t n, uint32_t magic) {
+  gd_randint d;
+  d.n = n;
+  d.magic = magic;
+  d.shift = 31u - (uint32_t)__clz((int)(n - 1u)); /* ceil(log2 n) - 1 */
+  const uint32_t q = (uint32_t)(((uint64_t)0x7FFFFFFFu * magic) >> 32) >> d.shift;
+  const uint32_t t = 0x7FFFFFFFu - q * n + 1u; /* (2^31 - 1) mod n + 1 */
+  d.limit = GD_RAND_MAX - (t == n ? 0u : t);
+  return d;
 }
 
 /* Fisher-Yates swaps of random_shuffle (css.c:700-706) on the lane's column, draws
  * from state x (no rejection: the caller checks); returns true if a draw would have
- * been rejected */
-__device__ __forceinline__ bool fy_fast(uint8_t *col, uint64_t x, int m, const gd_randint *rdt) {
+ * been rejected.  The next step's magic is read one step ahead. */
+__device__ __forceinline__ bool fy_fast(uint8_t *col, uint64_t x, int m, const uint32_t *mag) {
   bool rej = false;
+  uint32_t mg = __builtin_amdgcn_readfirstlane(mag[m]);
   for (int s = 0; s < m - 1; ++s) {
-    const int n = m - s;
+    const int n = __builtin_amdgcn_readfirstlane(m - s); /* wave-uniform */
+    const gd_randint rd = perm_rd((uint32_t)n, mg);
+    mg = __builtin_amdgcn_readfirstlane(mag[n - 1]);
     x = gd_lcg_next(x);
     const uint32_t r = gd_lcg_value(x);
-    const gd_randint rd = rdt[n];
     rej |= r > rd.limit;
     const int j = (int)gd_randint_mod(&rd, r);
-    const uint8_t u = col[(n - 1) * 64], v = col[j * 64];
-    col[(n - 1) * 64] = v;
-    col[j * 64] = u;
+    const uint8_t u = col[(n - 1) * PERM_ROW], v = col[j * PERM_ROW];
+    col[(n - 1) * PERM_ROW] = v;
+    col[j * PERM_ROW] = u;
   }
   return rej;
 }
 
 /* the same with random_int_nrand48's redraw loop (css.c:675-690) */
-__device__ __forceinline__ void fy_exact(uint8_t *col, uint64_t x, int m, const gd_randint *rdt) {
+__device__ __forceinline__ void fy_exact(uint8_t *col, uint64_t x, int m, const uint32_t *mag) {
   for (int s = 0; s < m - 1; ++s) {
-    const int n = m - s;
-    const gd_randint rd = rdt[n];
+    const int n = __builtin_amdgcn_readfirstlane(m - s);
+    const gd_randint rd = perm_rd((uint32_t)n, __builtin_amdgcn_readfirstlane(mag[n]));
     uint32_t r;
     do {
       x = gd_lcg_next(x);
       r = gd_lcg_value(x);
     } while (r > rd.limit);
     const int j = (int)gd_randint_mod(&rd, r);
-    const uint8_t u = col[(n - 1) * 64], v = col[j * 64];
-    col[(n - 1) * 64] = v;
-    col[j * 64] = u;
+    const uint8_t u = col[(n - 1) * PERM_ROW], v = col[j * PERM_ROW];
+    col[(n - 1) * PERM_ROW] = v;
+    col[j * PERM_ROW] = u;
   }
 }
 
@@ -250,21 +389,23 @@ __device__ __forceinline__ void fy_exact(uint8_t *col, uint64_t x, int m, const 
 template <int MP>
 __global__ void __launch_bounds__(PermShape<MP>::NT) PERM_WPE
     k_css_perm(const gd_chrom_dev *ch, int nchrom, const double *xbuf, const uint8_t *status, int64_t wtotal,
-               int treshold, int runs, double *pvals, unsigned *wq) {
-  constexpr int TRI = PermShape<MP>::TRI, NWV = PermShape<MP>::NWV, NT = PermShape<MP>::NT, P = 64 * NWV;
-  constexpr int SIG = MP * 64; /* one wave's byte matrix */
-  __shared__ double s_S[TRI];
+               int treshold, int runs, double *pvals, unsigned *wq, int force_exact) {
+  using SH = PermShape<MP>;
+  constexpr int TRI = SH::TRI, NWV = SH::NWV, NT = SH::NT, P = 64 * NWV, SIG = SH::SIG;
+  __shared__ __attribute__((aligned(16))) char s_U[SH::UBYTES];
+  __shared__ double s_X[2 * MP]; /* the window's MDS coordinates (FP64 distances on demand) */
   __shared__ double s_R[MP + 1];
-  __shared__ __attribute__((aligned(16))) uint8_t s_sig[NWV * SIG > 16 * MP ? NWV * SIG : 16 * MP];
-  __shared__ gd_randint s_rd[MP + 1];
-  __shared__ uint64_t s_st[P + 1];
   __shared__ uint64_t s_hit[NWV];
   __shared__ uint8_t s_car[MP > 64 ? 128 : 64];
   __shared__ int64_t s_w;
+  double *s_S = reinterpret_cast<double *>(s_U); /* FP64 triangle: window setup only */
+  float *s_S32 = reinterpret_cast<float *>(s_U);  /* FP32 triangle: the permutation passes */
+  uint64_t *s_st = reinterpret_cast<uint64_t *>(s_U + SH::OFF_MEM); /* serial start states (draw phase only) */
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  for (int n = tid; n <= MP; n += NT) s_rd[n] = gd_randint_make(n < 1 ? 1u : (uint32_t)n);
-  double *s_x = reinterpret_cast<double *>(s_sig); /* X staging, dead before the draws */
-  uint8_t *my_sig = s_sig + wave * SIG;
+  __shared__ uint32_t s_mag[MP + 1]; /* random_int_nrand48 magic numbers (perm_rd) */
+  for (int n = tid; n <= MP; n += NT) s_mag[n] = gd_randint_make(n < 1 ? 1u : (uint32_t)n).magic;
+  uint8_t *my_sig = reinterpret_cast<uint8_t *>(s_U + SH::OFF_SIG) + wave * SIG;
+  uint8_t *my_mem = reinterpret_cast<uint8_t *>(s_U + SH::OFF_MEM) + wave * SH::MEM;
 
   PERM_PROF_INIT;
   for (;;) {
@@ -282,12 +423,12 @@ __global__ void __launch_bounds__(PermShape<MP>::NT) PERM_WPE
     /* S (packed triangle, zero rows for individuals >= m) and its row sums */
     int ln = tid;
     PERM_OPAQUE(ln);
-    for (int e = ln; e < 2 * m; e += NT) s_x[e] = xbuf[w * 2 * MP + e];
+    for (int e = ln; e < 2 * m; e += NT) s_X[e] = xbuf[w * 2 * MP + e];
     __syncthreads();
 #pragma unroll 1
     for (int h = 1; h <= MP; ++h) {
       for (int l = ln; l < h; l += NT)
-        s_S[h * (h - 1) / 2 + l] = (h < m && l < m) ? perm_xdist(s_x, h, l) : 0.0;
+        s_S[h * (h - 1) / 2 + l] = (h < m && l < m) ? perm_xdist(s_X, h, l) : 0.0;
     }
     if (tid == 0) s_S[TRI - 1] = 0.0;
     __syncthreads();
@@ -305,9 +446,36 @@ __global__ void __launch_bounds__(PermShape<MP>::NT) PERM_WPE
 
     const double inva = a > 1 ? 1.0 / (double)(a * a * (a - 1)) : 0.0;
     const double invb = b > 1 ? 1.0 / (double)(b * b * (b - 1)) : 0.0;
-    sig_identity(my_sig, m, lane);
-    __syncthreads();
-    const double obs = perm_score<MP>(s_S, s_R, my_sig, lane, a, b, inva, invb);
+    /* the observed score: identity tracks, from the FP64 triangle */
+    const int g = a <= b ? a : b, goff = a <= b ? 0 : a;
+    const double obs = score_exact<MP, true>(
+        [](int k) { return (uint32_t)k; },
+        [&](int k) { return k < g ? (uint32_t)(goff + k) : (uint32_t)MP; },
+        [&](uint32_t x, uint32_t y) {
+          return *reinterpret_cast<const double *>(reinterpret_cast<const char *>(s_S) + tri8(y) + (x << 3));
+        },
+        s_R, a, b, inva, invb);
+    /* FP32 copy of the triangle over the head of the FP64 one, in chunks (the FP32
+     * entries of chunk j overlap only FP64 entries of chunks <= j, read before) */
+    {
+      constexpr int CH = 8;
+#pragma unroll 1
+      for (int e0 = 0; e0 < TRI; e0 += CH * NT) {
+        float v[CH];
+#pragma unroll
+        for (int i = 0; i < CH; ++i) {
+          const int e = e0 + i * NT + ln;
+          v[i] = e < TRI ? (float)s_S[e] : 0.f;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < CH; ++i) {
+          const int e = e0 + i * NT + ln;
+          if (e < TRI) s_S32[e] = v[i];
+        }
+        __syncthreads();
+      }
+    }
     PERM_PROF(0);
 
     uint64_t base = gd_window_state(d.seed, GD_STREAM_CSS, wl);
@@ -322,7 +490,7 @@ __global__ void __launch_bounds__(PermShape<MP>::NT) PERM_WPE
       int lq = lane;
       PERM_OPAQUE(lq);
       uint8_t *col = my_sig + lq;
-      const bool rej = fy_fast(col, gd_affine_apply(Jq, base), m, s_rd);
+      const bool rej = fy_fast(col, gd_affine_apply(Jq, base), m, s_mag);
       if (__syncthreads_or(rej)) {
         /* exact serial stream: the start state of every permutation of the pass */
         if (tid == 0) {
@@ -330,7 +498,7 @@ __global__ void __launch_bounds__(PermShape<MP>::NT) PERM_WPE
           for (int q = 0; q < P; ++q) {
             s_st[q] = y;
             for (int s = 0; s < m1; ++s) {
-              const gd_randint rd = s_rd[m - s];
+              const gd_randint rd = perm_rd((uint32_t)(m - s), s_mag[m - s]);
               do y = gd_lcg_next(y);
               while (gd_lcg_value(y) > rd.limit);
             }
@@ -340,7 +508,7 @@ __global__ void __launch_bounds__(PermShape<MP>::NT) PERM_WPE
         __syncthreads();
         sig_identity(my_sig, m, lane);
         __syncthreads();
-        fy_exact(col, s_st[tid], m, s_rd);
+        fy_exact(col, s_st[tid], m, s_mag);
         base = s_st[P];
       } else {
         base = gd_affine_apply(JP, base);
@@ -360,9 +528,11 @@ __global__ void __launch_bounds__(PermShape<MP>::NT) PERM_WPE
           uint32_t car = (uint32_t)s_car[li] | (MP > 64 ? (uint32_t)s_car[li + 64] << 8 : 0u);
 #pragma unroll
           for (int q = 0; q < 16; ++q) {
-            pf0[q] = r0 ? *reinterpret_cast<const uint32_t *>(my_sig + li * 64 + 4 * q) : 0u;
-            pf1[q] = r1 ? *reinterpret_cast<const uint32_t *>(my_sig + (li + 64) * 64 + 4 * q) : 0u;
+            pf0[q] = r0 ? *reinterpret_cast<const uint32_t *>(my_sig + li * PERM_ROW + 4 * q) : 0u;
+            pf1[q] = r1 ? *reinterpret_cast<const uint32_t *>(my_sig + (li + 64) * PERM_ROW + 4 * q) : 0u;
           }
+          /* F_q(i) for q = t .. t+3 leave as one dword per row (bytes t .. t+3 of row i) */
+          uint32_t w0 = 0, w1 = 0;
 #pragma unroll
           for (int t = 0; t < 64; ++t) {
             const uint32_t s0 = (pf0[t >> 2] >> (8 * (t & 3))) & 0xFFu;
@@ -373,11 +543,17 @@ __global__ void __launch_bounds__(PermShape<MP>::NT) PERM_WPE
               const uint32_t a1 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((s1 & 63u) << 2), (int)car);
               n0 = (s0 < 64 ? a0 : a0 >> 8) & 0xFFu;
               n1 = (s1 < 64 ? a1 : a1 >> 8) & 0xFFu;
-              if (r1) my_sig[(li + 64) * 64 + t] = (uint8_t)n1;
+              w1 |= n1 << (8 * (t & 3));
             } else {
               n0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(s0 << 2), (int)car);
             }
-            if (r0) my_sig[li * 64 + t] = (uint8_t)n0;
+            w0 |= n0 << (8 * (t & 3));
+            if ((t & 3) == 3) {
+              if (r0) *reinterpret_cast<uint32_t *>(my_sig + li * PERM_ROW + (t & ~3)) = w0;
+              if (MP > 64 && r1) *reinterpret_cast<uint32_t *>(my_sig + (li + 64) * PERM_ROW + (t & ~3)) = w1;
+              w0 = 0;
+              w1 = 0;
+            }
             car = n0 | (n1 << 8);
           }
           if (r0) s_car[li] = (uint8_t)car;
@@ -387,14 +563,34 @@ __global__ void __launch_bounds__(PermShape<MP>::NT) PERM_WPE
       }
 
       PERM_PROF(2);
-      /* 3. scores of the P permuted track arrays, 4. in-order hit count */
-      const double sc = perm_score<MP>(s_S, s_R, my_sig, lane, a, b, inva, invb);
+      /* 3. scores of the P permuted track arrays from the FP32 triangle; a lane whose
+       * estimate lies within its error bound of obs recomputes the FP64 score with S
+       * from the coordinates (the same values the FP64 triangle held), so every hit is
+       * decided exactly as score_exact decides it.  4. in-order hit count */
+      int lc = lane;
+      PERM_OPAQUE(lc);
+      const uint8_t *tcol = my_sig + lc;
+      uint8_t *mcol = my_mem + lc;
+      double est, err;
+      score_f32<MP>(s_S32, s_R, tcol, mcol, a, b, inva, invb, est, err);
+      if (force_exact) err = __builtin_inf();
+      int hit = est - obs > err ? 1 : (obs - est > err ? 0 : -1);
+      if (__any(hit < 0)) {
+        if (hit < 0) {
+          const double sc = score_exact<MP, false>(
+              [&](int k) { return (uint32_t)tcol[k * PERM_ROW]; },
+              [&](int k) { return k < g ? (uint32_t)mcol[k * 64] : (uint32_t)MP; },
+              [&](uint32_t x, uint32_t y) { return y < (uint32_t)m ? perm_xdist(s_X, (int)y, (int)x) : 0.0; }, s_R,
+              a, b, inva, invb);
+          hit = sc >= obs;
+        }
+      }
 #ifdef GD_PERM_PROFILE
       __syncthreads();
       PERM_PROF(3);
 #endif
       const int valid = min(P, runs - nsc);
-      const uint64_t H = __ballot(tid < valid && sc >= obs);
+      const uint64_t H = __ballot(tid < valid && hit > 0);
       if (lane == 0) s_hit[wave] = H;
       __syncthreads();
       for (int v = 0; v < NWV && !done; ++v) {
@@ -422,9 +618,13 @@ __global__ void __launch_bounds__(PermShape<MP>::NT) PERM_WPE
 template <int MP>
 static int launch_perm(const gd_chrom_dev *d_ch, int nchrom, const double *xbuf, const uint8_t *status, int64_t wtotal,
                        int treshold, int runs, double *p, unsigned *wq, hipStream_t s) {
+  /* GD_PERM_EXACT=1: every permuted score in FP64 (checks that the FP32 pre-filter
+   * changes no p-value) */
+  const char *fe = getenv("GD_PERM_EXACT");
+  const int force_exact = fe && fe[0] == '1' ? 1 : 0;
   const unsigned grid = (unsigned)std::min<int64_t>(wtotal, 256 * 16);
   hipLaunchKernelGGL(k_css_perm<MP>, dim3(grid), dim3(PermShape<MP>::NT), 0, s, d_ch, nchrom, xbuf, status, wtotal,
-                     treshold, runs, p, wq);
+                     treshold, runs, p, wq, force_exact);
   return hipGetLastError() == hipSuccess ? GD_OK : GD_ERR_HIP;
 }
 

@@ -200,3 +200,26 @@ def test_serial_window_set_with_permutations(oracle):
     s_ref, p_ref = oracle_css_scan(oracle, av, bv, ap, bp, regend, treshold=10, runs=200, seed=9, serial=True)
     _cmp_scores(s, s_ref)
     assert (p[s_ref != 0] == p_ref[s_ref != 0]).mean() >= 0.995
+
+
+@pytest.mark.parametrize("asize,bsize,treshold,runs,nsnp,dup", [(10, 10, 100_000, 500, 15_000, False),
+                                                                (40, 40, 100_000, 300, 3_000, False),
+                                                                (6, 9, 100_000, 1000, 10_000, True),
+                                                                (40, 40, 10, 1000, 3_000, True)])
+def test_fp32_prefilter_changes_no_p(asize, bsize, treshold, runs, nsnp, dup, monkeypatch):
+    """The permutation kernel decides hits from the FP32 copy of S and recomputes in
+    FP64 only where the estimate is within its error bound of the observed score;
+    GD_PERM_EXACT=1 scores every permutation in FP64.  The p-values must be identical,
+    including windows full of exact ties (duplicated individuals)."""
+    from gdscan import css
+    av, bv, ap, bp, regend = _synth(8, nsnp, asize, bsize)
+    if dup:
+        for arr, size in ((av, asize), (bv, bsize)):
+            v = arr.reshape(-1, size)
+            v[:, 1::2] = v[:, 0:size - 1:2][:, :v[:, 1::2].shape[1]]
+    s, p = css.scan(av, bv, ap, bp, regend, treshold=treshold, runs=runs, seed=5)
+    monkeypatch.setenv("GD_PERM_EXACT", "1")
+    s2, p2 = css.scan(av, bv, ap, bp, regend, treshold=treshold, runs=runs, seed=5)
+    assert np.array_equal(s, s2)
+    assert (s != 0).sum() > 10
+    assert np.array_equal(p, p2), np.flatnonzero(p != p2)[:10]
