@@ -436,8 +436,19 @@ __global__ void __launch_bounds__(PermShape<MP>::NT) PERM_WPE
       double acc = 0.0;
       if (r < m) {
         const uint32_t tr = tri8((uint32_t)r);
-        for (int j = 0; j < m; ++j)
-          if (j != r) acc += s_pair(s_S, (uint32_t)r, tr, (uint32_t)j, tri8((uint32_t)j));
+        /* j ascending, eight loads in flight */
+#pragma unroll 1
+        for (int j0 = 0; j0 < m; j0 += 8) {
+          double e[8];
+#pragma unroll
+          for (int t = 0; t < 8; ++t) {
+            const int j = j0 + t;
+            e[t] = j < m ? s_pair(s_S, (uint32_t)r, tr, (uint32_t)j, tri8((uint32_t)j)) : 0.0;
+          }
+#pragma unroll
+          for (int t = 0; t < 8; ++t)
+            if (j0 + t < m && j0 + t != r) acc += e[t];
+        }
       }
       s_R[r] = acc;
     }

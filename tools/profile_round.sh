@@ -20,5 +20,8 @@ timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES SQ_INSTS_SALU SQ_INSTS_
 timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES -d $O/pmc_css_valu -o run --output-format csv -- \
     python3 bench.py --steps 1 --warmup 0 --no-cpu --css-steps 1 --no-extra > $O/pmc_css_valu.json 2> $O/pmc_css_valu.err &&
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $O/pmc_css_fetch -o run --output-format csv -- \
-    python3 bench.py --steps 1 --warmup 0 --no-cpu --css-steps 1 --no-extra > $O/pmc_css.json 2> $O/pmc_css.err
+    python3 bench.py --steps 1 --warmup 0 --no-cpu --css-steps 1 --no-extra > $O/pmc_css.json 2> $O/pmc_css.err &&
+POP=40 NCH=1 RUNS=1000 TRES=10 STEPS=1 timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS \
+    SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES -d $O/pmc_perm -o run \
+    --output-format csv -- python3 tools/css_time.py > $O/pmc_perm.txt 2> $O/pmc_perm.err
 echo "profile_round exit $?"
