@@ -26,6 +26,7 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <cstdio>
 #include <cstdlib>
 
 #include "../../include/gdscan.h"
@@ -381,6 +382,9 @@ __device__ __forceinline__ void fy_exact(uint8_t *col, uint64_t x, int m, const 
 
 }  // namespace
 
+#ifdef PERM_COUNT_AMBIGUOUS
+__device__ unsigned long long g_perm_amb[2];
+#endif
 #ifdef PERM_WAVES_PER_SIMD /* diagnostic: register-allocation target */
 #define PERM_WPE __attribute__((amdgpu_waves_per_eu(PERM_WAVES_PER_SIMD, PERM_WAVES_PER_SIMD)))
 #else
@@ -586,6 +590,10 @@ __global__ void __launch_bounds__(PermShape<MP>::NT) PERM_WPE
       score_f32<MP>(s_S32, s_R, tcol, mcol, a, b, inva, invb, est, err);
       if (force_exact) err = __builtin_inf();
       int hit = est - obs > err ? 1 : (obs - est > err ? 0 : -1);
+#ifdef PERM_COUNT_AMBIGUOUS /* diagnostics: ambiguous lanes and wave-passes that ran the FP64 path */
+      if (hit < 0) atomicAdd(&g_perm_amb[0], 1ull);
+      if (__any(hit < 0) && lane == 0) atomicAdd(&g_perm_amb[1], 1ull);
+#endif
       if (__any(hit < 0)) {
         if (hit < 0) {
           const double sc = score_exact<MP, false>(
@@ -656,6 +664,17 @@ int gd_css_perm_launch(int mp, const gd_chrom_dev *d_ch, int nchrom, const doubl
               h[3], h[4]);
     }
   } dump{s};
+#endif
+#ifdef PERM_COUNT_AMBIGUOUS
+  struct DumpAmb {
+    hipStream_t s;
+    ~DumpAmb() {
+      unsigned long long h[2];
+      (void)hipStreamSynchronize(s);
+      (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(g_perm_amb), sizeof h);
+      fprintf(stderr, "perm ambiguous lanes %llu, wave-passes with an FP64 recompute %llu (cumulative)\n", h[0], h[1]);
+    }
+  } dump_amb{s};
 #endif
   switch (mp) {
     case 24: return launch_perm<24>(d_ch, nchrom, xbuf, status, wtotal, treshold, runs, p, wq, s);

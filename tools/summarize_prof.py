@@ -95,6 +95,22 @@ if mds and ncv.get("k_css_pack", 0):
                          "per call = per C3 scan)"}
     (dst / f"{R}_css_valu.json").write_text(json.dumps(css_doc, indent=1) + "\n")
 
+# CSS permutations (C5 shape, tools/css_time.py): SQ counters of k_css_perm per dispatch
+perm_doc = None
+if (src / "pmc_perm").exists():
+    pc = defaultdict(float)
+    pd = set()
+    for row in csv.DictReader(open(find(src / "pmc_perm", "counter_collection.csv"))):
+        if short(row["Kernel_Name"]).startswith("k_css_perm"):
+            pc[row["Counter_Name"]] += float(row["Counter_Value"])
+            pd.add(row["Dispatch_Id"])
+    if pd:
+        per = {k: v / len(pd) for k, v in pc.items()}
+        perm_doc = {"config": "1 chromosome x 500000 SNPs, 40+40, mcT=10, mcR=1000 (tools/css_time.py)",
+                    "per_dispatch": per,
+                    "method": "rocprofv3 --pmc SQ_* over k_css_perm<80> (one dispatch per scan)"}
+        (dst / f"{R}_perm_pmc.json").write_text(json.dumps(perm_doc, indent=1) + "\n")
+
 rows = list(csv.DictReader(open(stats)))
 lines = [f"# {R} profile summary", "", "Command: `rocprofv3 --kernel-trace --stats -- python3 bench.py --steps 5 "
          "--warmup 1 --no-cpu` (FET + CSS legs), PMC passes separate (tools/profile_round.sh).", "",
@@ -109,5 +125,8 @@ lines += ["", f"FET scan HBM traffic (PMC): {traffic['bytes_per_scan'] / 1e9:.3f
           f"per scan; at the bench's scan time that is {valu_doc['valu_wave_insts_per_scan'] / (bench['roofline']['stage_ms']['scan_total'] * 1e-3) / 1e9:.0f} "
           "G/s of the 614 G/s issue peak (256 CUs x 4 SIMDs x 2.4 GHz / 4).",
           "", "Bench line (same call):", "", "```", json.dumps(bench), "```"]
+if perm_doc:
+    lines[-5:-5] = ["", "k_css_perm<80> per dispatch (PMC): " + ", ".join(
+        f"{k} {v:.4g}" for k, v in sorted(perm_doc["per_dispatch"].items()))]
 (dst / f"{R}_summary.md").write_text("\n".join(lines) + "\n")
 print("\n".join(lines[:40]))
