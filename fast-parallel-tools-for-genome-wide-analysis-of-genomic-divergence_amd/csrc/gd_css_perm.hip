@@ -226,8 +226,9 @@ __device__ __forceinline__ double score_exact(TRK track, MEMB member, SXY sxy, c
  * at col[k*PERM_ROW]) and writes G's members ascending to `mcol` (the track stays intact
  * for score_exact).  sr, the row-sum term, is summed exactly as score_exact sums it. */
 template <int MP>
-__device__ __forceinline__ void score_f32(const float *S32, const double *R, const uint8_t *col, uint8_t *mcol, int a,
-                                          int b, double inva, double invb, double &est, double &err) {
+__device__ __forceinline__ void score_f32(const float *S32, const double *R, const uint8_t *col, const uint8_t *fmap,
+                                          bool mapped, uint8_t *mcol, int a, int b, double inva, double invb,
+                                          double &est, double &err) {
   constexpr int NB = (PermShape<MP>::HALF + 7) / 8;
   const int m = a + b;
   const int g = a <= b ? a : b, off = a <= b ? 0 : a;
@@ -240,11 +241,17 @@ __device__ __forceinline__ void score_f32(const float *S32, const double *R, con
     lo |= x < 64 ? 1ull << (x & 63u) : 0ull;
     if constexpr (MP > 64) hi |= x >= 64 ? 1ull << (x & 63u) : 0ull;
   };
-  uint32_t prev = col[0], tprev = tri4(prev);
+  /* track entry k: the column byte, through the wave's map when its compositions started
+   * from the identity (`mapped` is wave-uniform) */
+  auto track = [&](int k) -> uint32_t {
+    const uint32_t c = col[k * PERM_ROW];
+    return mapped ? (uint32_t)fmap[c] : c;
+  };
+  uint32_t prev = track(0), tprev = tri4(prev);
   if (off == 0 && g > 0) add_member(prev);
 #pragma unroll 4
   for (int k = 1; k < m; ++k) {
-    const uint32_t cur = col[k * PERM_ROW], tcur = tri4(cur);
+    const uint32_t cur = track(k), tcur = tri4(cur);
     const float e = s_at(prev > cur ? tprev + (cur << 2) : tcur + (prev << 2));
     if (k < a) wa += e;
     if (k > a) wb += e;
@@ -401,6 +408,8 @@ __global__ void __launch_bounds__(PermShape<MP>::NT) PERM_WPE
   __shared__ double s_R[MP + 1];
   __shared__ uint64_t s_hit[NWV];
   __shared__ uint8_t s_car[MP > 64 ? 128 : 64];
+  __shared__ uint8_t s_gend[NWV * MP]; /* each wave's last composition */
+  __shared__ uint8_t s_fs[NWV * MP];   /* wave v > 0: the tracks before its first permutation */
   __shared__ int64_t s_w;
   double *s_S = reinterpret_cast<double *>(s_U); /* FP64 triangle: window setup only */
   float *s_S32 = reinterpret_cast<float *>(s_U);  /* FP32 triangle: the permutation passes */
@@ -531,52 +540,68 @@ __global__ void __launch_bounds__(PermShape<MP>::NT) PERM_WPE
       __syncthreads();
       PERM_PROF(1);
 
-      /* 2. F_q = F_{q-1} o sigma_q, one wave after the other; lane i owns rows i and i + 64 */
-      for (int v = 0; v < NWV; ++v) {
-        if (wave == v) {
-          uint32_t pf0[16], pf1[16];
-          int li = lane;
-          PERM_OPAQUE(li);
-          const bool r0 = li < m, r1 = MP > 64 && li + 64 < m;
-          /* above 64 individuals lane i carries F(i) and F(i + 64) as the low two bytes of
-           * one word, so one ds_bpermute per row fetches whichever of the two is wanted */
-          uint32_t car = (uint32_t)s_car[li] | (MP > 64 ? (uint32_t)s_car[li + 64] << 8 : 0u);
+      /* 2. compositions, all waves at once; lane i owns rows i and i + 64.  Wave 0 composes
+       * F_q = F_{q-1} o sigma_q from the carried tracks; wave v > 0 composes
+       * G_t = G_{t-1} o sigma_{64v+t} from the identity, and its tracks are
+       * F_{64v+t} = Fs_v o G_t with Fs_v = F_{64v-1}, read through the map s_fs[v] */
+      {
+        uint32_t pf0[16], pf1[16];
+        int li = lane;
+        PERM_OPAQUE(li);
+        const bool r0 = li < m, r1 = MP > 64 && li + 64 < m;
+        /* above 64 individuals lane i carries F(i) and F(i + 64) as the low two bytes of
+         * one word, so one ds_bpermute per row fetches whichever of the two is wanted */
+        uint32_t car = wave == 0 ? (uint32_t)s_car[li] | (MP > 64 ? (uint32_t)s_car[li + 64] << 8 : 0u)
+                                 : (uint32_t)li | (MP > 64 ? (uint32_t)(li + 64) << 8 : 0u);
 #pragma unroll
-          for (int q = 0; q < 16; ++q) {
-            pf0[q] = r0 ? *reinterpret_cast<const uint32_t *>(my_sig + li * PERM_ROW + 4 * q) : 0u;
-            pf1[q] = r1 ? *reinterpret_cast<const uint32_t *>(my_sig + (li + 64) * PERM_ROW + 4 * q) : 0u;
-          }
-          /* F_q(i) for q = t .. t+3 leave as one dword per row (bytes t .. t+3 of row i) */
-          uint32_t w0 = 0, w1 = 0;
-#pragma unroll
-          for (int t = 0; t < 64; ++t) {
-            const uint32_t s0 = (pf0[t >> 2] >> (8 * (t & 3))) & 0xFFu;
-            uint32_t n0, n1 = 0;
-            if constexpr (MP > 64) {
-              const uint32_t s1 = (pf1[t >> 2] >> (8 * (t & 3))) & 0xFFu;
-              const uint32_t a0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((s0 & 63u) << 2), (int)car);
-              const uint32_t a1 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((s1 & 63u) << 2), (int)car);
-              n0 = (s0 < 64 ? a0 : a0 >> 8) & 0xFFu;
-              n1 = (s1 < 64 ? a1 : a1 >> 8) & 0xFFu;
-              w1 |= n1 << (8 * (t & 3));
-            } else {
-              n0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(s0 << 2), (int)car);
-            }
-            w0 |= n0 << (8 * (t & 3));
-            if ((t & 3) == 3) {
-              if (r0) *reinterpret_cast<uint32_t *>(my_sig + li * PERM_ROW + (t & ~3)) = w0;
-              if (MP > 64 && r1) *reinterpret_cast<uint32_t *>(my_sig + (li + 64) * PERM_ROW + (t & ~3)) = w1;
-              w0 = 0;
-              w1 = 0;
-            }
-            car = n0 | (n1 << 8);
-          }
-          if (r0) s_car[li] = (uint8_t)car;
-          if (r1) s_car[li + 64] = (uint8_t)(car >> 8);
+        for (int q = 0; q < 16; ++q) {
+          pf0[q] = r0 ? *reinterpret_cast<const uint32_t *>(my_sig + li * PERM_ROW + 4 * q) : 0u;
+          pf1[q] = r1 ? *reinterpret_cast<const uint32_t *>(my_sig + (li + 64) * PERM_ROW + 4 * q) : 0u;
         }
-        __syncthreads();
+        /* F_q(i) for q = t .. t+3 leave as one dword per row (bytes t .. t+3 of row i) */
+        uint32_t w0 = 0, w1 = 0;
+#pragma unroll
+        for (int t = 0; t < 64; ++t) {
+          const uint32_t s0 = (pf0[t >> 2] >> (8 * (t & 3))) & 0xFFu;
+          uint32_t n0, n1 = 0;
+          if constexpr (MP > 64) {
+            const uint32_t s1 = (pf1[t >> 2] >> (8 * (t & 3))) & 0xFFu;
+            const uint32_t a0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((s0 & 63u) << 2), (int)car);
+            const uint32_t a1 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((s1 & 63u) << 2), (int)car);
+            n0 = (s0 < 64 ? a0 : a0 >> 8) & 0xFFu;
+            n1 = (s1 < 64 ? a1 : a1 >> 8) & 0xFFu;
+            w1 |= n1 << (8 * (t & 3));
+          } else {
+            n0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(s0 << 2), (int)car);
+          }
+          w0 |= n0 << (8 * (t & 3));
+          if ((t & 3) == 3) {
+            if (r0) *reinterpret_cast<uint32_t *>(my_sig + li * PERM_ROW + (t & ~3)) = w0;
+            if (MP > 64 && r1) *reinterpret_cast<uint32_t *>(my_sig + (li + 64) * PERM_ROW + (t & ~3)) = w1;
+            w0 = 0;
+            w1 = 0;
+          }
+          car = n0 | (n1 << 8);
+        }
+        /* the wave's last composition: F_{63} (wave 0) or G_{63} (wave v > 0) */
+        uint8_t *gend = s_gend + wave * MP;
+        if (r0) gend[li] = (uint8_t)car;
+        if (r1) gend[li + 64] = (uint8_t)(car >> 8);
       }
-
+      __syncthreads();
+      /* the chain across the waves: Fs_1 = F_63, Fs_v = Fs_{v-1} o G^{v-1}_63, and the
+       * carry into the next pass Fs_{NWV-1} o G^{NWV-1}_63 (NWV - 1 small compositions) */
+      if (wave == 0) {
+        /* wave 0 alone, LDS in issue order: each step reads what the previous one wrote */
+        for (int v = 1; v < NWV; ++v) {
+          for (int i = lane; i < m; i += 64)
+            s_fs[v * MP + i] = v == 1 ? s_gend[i] : s_fs[(v - 1) * MP + s_gend[(v - 1) * MP + i]];
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        }
+        for (int i = lane; i < m; i += 64)
+          s_car[i] = NWV == 1 ? s_gend[i] : s_fs[(NWV - 1) * MP + s_gend[(NWV - 1) * MP + i]];
+      }
+      __syncthreads();
       PERM_PROF(2);
       /* 3. scores of the P permuted track arrays from the FP32 triangle; a lane whose
        * estimate lies within its error bound of obs recomputes the FP64 score with S
@@ -587,7 +612,9 @@ __global__ void __launch_bounds__(PermShape<MP>::NT) PERM_WPE
       const uint8_t *tcol = my_sig + lc;
       uint8_t *mcol = my_mem + lc;
       double est, err;
-      score_f32<MP>(s_S32, s_R, tcol, mcol, a, b, inva, invb, est, err);
+      const bool mapped = __builtin_amdgcn_readfirstlane(wave) > 0;
+      const uint8_t *fmap = s_fs + __builtin_amdgcn_readfirstlane(wave) * MP;
+      score_f32<MP>(s_S32, s_R, tcol, fmap, mapped, mcol, a, b, inva, invb, est, err);
       if (force_exact) err = __builtin_inf();
       int hit = est - obs > err ? 1 : (obs - est > err ? 0 : -1);
 #ifdef PERM_COUNT_AMBIGUOUS /* diagnostics: ambiguous lanes and wave-passes that ran the FP64 path */
@@ -597,7 +624,10 @@ __global__ void __launch_bounds__(PermShape<MP>::NT) PERM_WPE
       if (__any(hit < 0)) {
         if (hit < 0) {
           const double sc = score_exact<MP, false>(
-              [&](int k) { return (uint32_t)tcol[k * PERM_ROW]; },
+              [&](int k) {
+                const uint32_t c = tcol[k * PERM_ROW];
+                return mapped ? (uint32_t)fmap[c] : c;
+              },
               [&](int k) { return k < g ? (uint32_t)mcol[k * 64] : (uint32_t)MP; },
               [&](uint32_t x, uint32_t y) { return y < (uint32_t)m ? perm_xdist(s_X, (int)y, (int)x) : 0.0; }, s_R,
               a, b, inva, invb);
