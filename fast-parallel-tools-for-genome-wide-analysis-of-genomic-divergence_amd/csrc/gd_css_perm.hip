@@ -247,17 +247,32 @@ __device__ __forceinline__ void score_f32(const float *S32, const double *R, con
     const uint32_t c = col[k * PERM_ROW];
     return mapped ? (uint32_t)fmap[c] : c;
   };
+  /* split at the group boundary (G is group A iff ga, wave-uniform): no per-entry selects */
+  const bool ga = off == 0;
   uint32_t prev = track(0), tprev = tri4(prev);
-  if (off == 0 && g > 0) add_member(prev);
-#pragma unroll 4
-  for (int k = 1; k < m; ++k) {
-    const uint32_t cur = track(k), tcur = tri4(cur);
+  auto pair_next = [&](uint32_t cur, uint32_t tcur) {
     const float e = s_at(prev > cur ? tprev + (cur << 2) : tcur + (prev << 2));
-    if (k < a) wa += e;
-    if (k > a) wb += e;
-    if (k >= off && k < off + g) add_member(cur);
     prev = cur;
     tprev = tcur;
+    return e;
+  };
+  if (ga && g > 0) add_member(prev);
+#pragma unroll 4
+  for (int k = 1; k < a; ++k) {
+    const uint32_t cur = track(k);
+    wa += pair_next(cur, tri4(cur));
+    if (ga) add_member(cur);
+  }
+  if (a > 0 && a < m) { /* the pair across the boundary counts for neither group */
+    prev = track(a);
+    tprev = tri4(prev);
+    if (!ga) add_member(prev);
+  }
+#pragma unroll 4
+  for (int k = a + 1; k < m; ++k) {
+    const uint32_t cur = track(k);
+    wb += pair_next(cur, tri4(cur));
+    if (!ga) add_member(cur);
   }
   /* the members, ascending */
 #pragma unroll 4
