@@ -1,67 +1,11 @@
-"""CPU restatements of three pieces of the CSS permutation kernel (gd_css_perm.hip) that
+"""CPU restatements of two pieces of the CSS permutation kernel (gd_css_perm.hip) that
 are not visible in its outputs on ordinary data, checked against their definitions:
 
-* fy_fast's two-swaps-per-round Fisher-Yates (step n-1 reads take step n's writes where
-  they alias) == random_shuffle's sequential swaps (css.c:700-706) for every draw sequence;
 * perm_rd's limit and shift from the magic number alone == gd_randint_make's
   (random_int_nrand48, css.c:675-690) for every n in 2..128;
 * score_f32's error bound: a sum of n FP32-rounded non-negative terms lies within
   (n + 2) 2^-24 (1.001) of its computed value."""
-import random
-
 import numpy as np
-
-
-def _fy_sequential(m, js):
-    col = list(range(m))
-    for s in range(m - 1):
-        n = m - s
-        j = js[s]
-        col[n - 1], col[j] = col[j], col[n - 1]
-    return col
-
-
-def _fy_two_step(m, js):
-    col = list(range(m))
-    s = 0
-    while s + 2 <= m - 1:
-        n = m - s
-        ja, jb = js[s], js[s + 1]
-        ua, va, ub, vb = col[n - 1], col[ja], col[n - 2], col[jb]
-        if ja == n - 2:
-            ub = ua
-        if jb == ja:
-            vb = ua
-        if jb == n - 2:
-            vb = ub
-        col[n - 1] = va
-        col[ja] = ua
-        col[n - 2] = vb
-        col[jb] = ub
-        s += 2
-    if s < m - 1:
-        n = m - s
-        j = js[s]
-        col[n - 1], col[j] = col[j], col[n - 1]
-    return col
-
-
-def test_two_step_fisher_yates_equals_sequential():
-    rng = random.Random(1)
-    for _ in range(50_000):
-        m = rng.randint(2, 14)
-        js = [rng.randint(0, m - s - 1) for s in range(m - 1)]
-        assert _fy_two_step(m, js) == _fy_sequential(m, js), (m, js)
-    # every aliasing pattern of one round at small m, exhaustively
-    for m in range(2, 7):
-        def rec(prefix):
-            s = len(prefix)
-            if s == m - 1:
-                assert _fy_two_step(m, prefix) == _fy_sequential(m, prefix)
-                return
-            for j in range(m - s):
-                rec(prefix + [j])
-        rec([])
 
 
 def test_divisor_constants_from_magic():
