@@ -370,14 +370,16 @@ __device__ __forceinline__ gd_randint perm_rd(uint32_t n, uint32_t magic) {
 __device__ __forceinline__ bool fy_fast(uint8_t *col, uint64_t x, int m, const uint32_t *mag) {
   bool rej = false;
   uint32_t mg = __builtin_amdgcn_readfirstlane(mag[m]);
+  /* the LCG on y = x << 16 (mod 2^64): no 48-bit mask, the draw is y >> 33 */
+  uint64_t y = x << 16;
   for (int s = 0; s < m - 1; ++s) {
     const int n = __builtin_amdgcn_readfirstlane(m - s); /* wave-uniform */
     const gd_randint rd = perm_rd((uint32_t)n, mg);
     mg = __builtin_amdgcn_readfirstlane(mag[n - 1]);
-    x = gd_lcg_next(x);
-    const uint32_t r = gd_lcg_value(x);
+    y = y * GD_LCG_A + (GD_LCG_C << 16);
+    const uint32_t r = (uint32_t)(y >> 33);
     rej |= r > rd.limit;
-    const int j = (int)gd_randint_mod(&rd, r);
+    const int j = (int)(r - (__umulhi(r, rd.magic) >> rd.shift) * (uint32_t)n); /* r mod n, n >= 2 */
     const uint8_t u = col[(n - 1) * PERM_ROW], v = col[j * PERM_ROW];
     col[(n - 1) * PERM_ROW] = v;
     col[j * PERM_ROW] = u;
