@@ -1213,6 +1213,23 @@ __device__ __forceinline__ double quad_sum(double x) {
   return x + dpp64<0x4E, 0xF>(x, 0.0); /* quad_perm [2,3,0,1] */
 }
 
+/* Row K, v and w reach the main rows as LDS broadcasts (every lane reads the same
+ * doubles: 64 x 8 B of LDS return bandwidth per double), or, with these switches, by
+ * v_readlane from the lane that holds them (two VALU per double, SGPR operands). */
+#ifndef T80_RL_ROW
+#define T80_RL_ROW 0
+#endif
+#ifndef T80_RL_VW
+#define T80_RL_VW 0
+#endif
+template <int K>
+__device__ __forceinline__ double t80_row(const double (&A)[T80], const double *s_row, int j) {
+#if T80_RL_ROW
+  if constexpr (K < T80_MAIN) return readlane_f64(A[j], K);
+#endif
+  return s_row[j];
+}
+
 /* One Householder step (hh_step_static) over the main rows and the LDS tail. */
 template <int K>
 __device__ __forceinline__ void t80_step(double (&A)[T80], int m, double *s_row, double *s_v, double *s_w,
@@ -1254,8 +1271,8 @@ __device__ __forceinline__ void t80_step(double (&A)[T80], int m, double *s_row,
       if (8 * jb + 7 > K) {
 #pragma unroll
         for (int u = 0; u < 8; u += 2) {
-          if (8 * jb + u > K) p0 = fma(A[8 * jb + u], s_row[8 * jb + u], p0);
-          if (8 * jb + u + 1 > K) p1 = fma(A[8 * jb + u + 1], s_row[8 * jb + u + 1], p1);
+          if (8 * jb + u > K) p0 = fma(A[8 * jb + u], t80_row<K>(A, s_row, 8 * jb + u), p0);
+          if (8 * jb + u + 1 > K) p1 = fma(A[8 * jb + u + 1], t80_row<K>(A, s_row, 8 * jb + u + 1), p1);
         }
         CSS_PIN(p0);
         CSS_PIN(p1);
@@ -1326,7 +1343,18 @@ __device__ __forceinline__ void t80_step(double (&A)[T80], int m, double *s_row,
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
           const int j = 8 * jb + u;
-          if (j > K) A[j] = fma(-vi, s_w[j], fma(-wi, s_v[j], A[j]));
+          if (j > K) {
+#if T80_RL_VW
+            /* v_j, w_j from the lane that computed them (row j < 64: lane j; tail row j:
+             * lane 4 (j - 64)) as SGPR operands instead of LDS broadcasts */
+            const int src = j < T80_MAIN ? j : 4 * (j - T80_MAIN);
+            const double wj = readlane_f64(j < T80_MAIN ? wi : wt, src);
+            const double vj = readlane_f64(j < T80_MAIN ? vi : vt, src);
+#else
+            const double wj = s_w[j], vj = s_v[j];
+#endif
+            A[j] = fma(-vi, wj, fma(-wi, vj, A[j]));
+          }
         }
 #pragma unroll
         for (int u = 0; u < 8; ++u) CSS_PIN(A[8 * jb + u]);
