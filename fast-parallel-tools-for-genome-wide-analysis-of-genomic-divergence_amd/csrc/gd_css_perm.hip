@@ -455,10 +455,18 @@ __global__ void __launch_bounds__(PermShape<MP>::NT) PERM_WPE
     PERM_OPAQUE(ln);
     for (int e = ln; e < 2 * m; e += NT) s_X[e] = xbuf[w * 2 * MP + e];
     __syncthreads();
-#pragma unroll 1
-    for (int h = 1; h <= MP; ++h) {
-      for (int l = ln; l < h; l += NT)
-        s_S[h * (h - 1) / 2 + l] = (h < m && l < m) ? perm_xdist(s_X, h, l) : 0.0;
+    /* entry e = T(h) + l of the triangle, e strided over the threads (independent
+     * entries, no per-row loop): h from the float root of 8e + 1 (within one of the
+     * true row for e < 2^24), then corrected */
+#pragma unroll 4
+    for (int e = ln; e < TRI - 1; e += NT) {
+      int h = (int)((1.0f + __fsqrt_rn(8.0f * (float)e + 1.0f)) * 0.5f);
+      if (h * (h - 1) / 2 > e)
+        --h;
+      else if (h * (h + 1) / 2 <= e)
+        ++h;
+      const int l = e - h * (h - 1) / 2;
+      s_S[e] = (h < m && l < m) ? perm_xdist(s_X, h, l) : 0.0;
     }
     if (tid == 0) s_S[TRI - 1] = 0.0;
     __syncthreads();
