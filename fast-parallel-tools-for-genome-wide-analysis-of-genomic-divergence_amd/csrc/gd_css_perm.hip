@@ -274,18 +274,29 @@ __device__ __forceinline__ void score_f32(const float *S32, const double *R, con
     wb += pair_next(cur, tri4(cur));
     if (!ga) add_member(cur);
   }
-  /* the members, ascending */
-#pragma unroll 4
-  for (int k = 0; k < g; ++k) {
-    uint32_t x;
-    if (MP <= 64 || lo != 0) {
-      x = (uint32_t)__builtin_ctzll(lo);
-      lo &= lo - 1;
+  /* the members, ascending: the set bits of lo, then those of hi (per-lane trip counts;
+   * one find-first-set per member instead of both words' in every step) */
+  int k = 0;
+  while (lo != 0) {
+    mcol[k * 64] = (uint8_t)__builtin_ctzll(lo);
+    lo &= lo - 1;
+    ++k;
+  }
+  if constexpr (MP > 64) {
+    if constexpr (MP - 64 <= 32) {
+      uint32_t h = (uint32_t)hi;
+      while (h != 0) {
+        mcol[k * 64] = (uint8_t)(64u + (uint32_t)__builtin_ctz(h));
+        h &= h - 1;
+        ++k;
+      }
     } else {
-      x = 64u + (uint32_t)__builtin_ctzll(hi);
-      hi &= hi - 1;
+      while (hi != 0) {
+        mcol[k * 64] = (uint8_t)(64u + (uint32_t)__builtin_ctzll(hi));
+        hi &= hi - 1;
+        ++k;
+      }
     }
-    mcol[k * 64] = (uint8_t)x;
   }
   auto member = [&](int k) -> uint32_t { return k < g ? (uint32_t)mcol[k * 64] : (uint32_t)MP; };
   /* gathers in pairs, summed with packed FP32 adds (v_pk_add_f32) */
