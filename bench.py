@@ -1,31 +1,35 @@
 #!/usr/bin/env python3
-"""Benchmark: genome-wide FET window scan on MI355X (BASELINE.json configs[1]).
+"""Benchmark: genome-wide FET and CSS window scans on MI355X (BASELINE.json configs).
 
-One step = one device-resident FET scan (per-SNP Fisher exact test, window
-95th-percentile score, 100-replicate bootstrap stddev) over this rank's batch of
-synthetic chromosomes: 20 chromosomes x 500k SNPs, 20+20 individuals, 2.5 kb
-windows / 500 bp step  (10M SNPs, ~1M windows per GPU).  Inputs are generated on
-the device before timing; weak scaling: every rank scans its own 20 chromosomes
-(chromosome ids rank*20 .. rank*20+19), no data-path collective.
+Headline (`value`): one step = one device-resident FET scan (per-SNP Fisher exact test,
+window 95th-percentile score, 100-replicate bootstrap stddev) over this rank's batch of
+synthetic chromosomes: configs[1], 20 chromosomes x 500k SNPs, 20+20 individuals, 2.5 kb
+windows / 500 bp step (10M SNPs, ~1M windows per GPU).  Inputs are generated on the device
+before timing; weak scaling: rank r scans chromosome ids 20r .. 20r+19, no data-path
+collective; `value` = all ranks' windows / the max-over-ranks time.
 
-Prints ONE JSON line (rank 0).  `roofline` prices the whole scan's algorithmic
-HBM bytes B = 12*(alen+blen) + 16*W (f64 value + i32 position per
-genotype, two f64 outputs per window) against its kernel time, and also lists each
-stage's kernel time.  `traffic` is the measured HBM bytes per scan from the committed
-rocprofv3 PMC summary (profiles/r02_fet_traffic.json, FETCH_SIZE doubled per the
-gfx950 correction + WRITE_SIZE), or null when absent.  The scan is bound by VALU issue
-(the bootstrap's draws), not HBM: `roofline.valu` prices the PMC-counted VALU
-wave-instructions per scan (profiles/r02_fet_valu.json) over this run's scan time
-against the 614 G wave-instructions/s issue peak.  `cpu_baseline` times the
-reference's own Pthreads threadcompute() (oracle/_ref, compiled from the reference
-sources) on a bounded sample of the same workload, or the oracle port when that
-binary is absent.
+Launch: `python bench.py --gpus N`.  With N > 1 and no torch.distributed environment the
+script starts `torch.distributed.run` with N ranks (127.0.0.1) as a child process before
+anything touches the GPU, and exits with its code.  `--backend gloo --dry-run` runs the
+distributed plumbing (launcher, shard plans, the chromosome queue, the track gather) on
+the CPU with no GPU work (tests/test_bench_launch.py).
 
-A second object, `css`, measures the CSS scan (BASELINE.json configs[2]: 1M windows,
-20+20, classical MDS, runs=0) on the same resident chromosomes, priced against the
-FP64 roofline with SURVEY.md 8(d)'s solver-neutral (4/3) m^3 + 10 m^2 flops per
-window, with the CPU oracle port timed on a sample beside it (the reference CSS
-needs GSL, absent from the image, so no reference binary exists).
+Beside the headline (objects in the same JSON line):
+  roofline      the FET scan's algorithmic HBM bytes B = 12 (alen + blen) + 16 W per step
+                 over its kernel time (HIP events), measured traffic from
+                the committed PMC profile, and the VALU-issue figure that actually binds it
+  cpu_baseline  the reference's own threadcompute() (oracle/_ref, compiled from the
+                reference sources; 64 pthreads on the host's cores) on all 20 chromosomes,
+                plus `parity`: its scores against the GPU scores of the same windows
+  css           configs[2] (C3: the same 20 chromosomes, 20+20, classical MDS, runs=0), and
+  css.c4        configs[3] per-GPU share: 25 chromosomes x 500k SNPs per GPU at 40+40, runs=0,
+                sharded over ranks by plan_shards, (score, p) track all-gathered and timed
+  css.c5        configs[4] per-GPU share: the same at mcT=10, mcR=1000, chromosomes pulled
+                from a shared queue (store counter) since the early-exit permutations make
+                their cost data-dependent; permutation histogram and per-rank imbalance
+  Each CSS leg carries an FP64 roofline (SURVEY.md 8(d) flops), the VALU figure from the
+  committed PMC profile of the kernels it dispatches, and (N=1, rank 0) a cpu_baseline:
+  the oracle port threaded over the host's cores (the reference CSS needs GSL, absent).
 """
 from __future__ import annotations
 
@@ -33,6 +37,8 @@ import argparse
 import ctypes
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 from pathlib import Path
@@ -44,14 +50,24 @@ PKG = ROOT / "fast-parallel-tools-for-genome-wide-analysis-of-genomic-divergence
 sys.path.insert(0, str(PKG))
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, HBM3E spec
-FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 vector spec; ubench: ~31-37 T FMA/s
-PROFILE_ROUND = "r02"
-TRAFFIC_FILE = ROOT / "profiles" / f"{PROFILE_ROUND}_fet_traffic.json"
-VALU_FILE = ROOT / "profiles" / f"{PROFILE_ROUND}_fet_valu.json"
-CSS_VALU_FILE = ROOT / "profiles" / f"{PROFILE_ROUND}_css_valu.json"
-# VALU issue peak: 256 CUs x 4 SIMDs, one wave64 VALU instruction per 4 cycles per SIMD
-# at the 2.4 GHz max clock (MI355X_MICROARCH.md) = 614.4 G wave-instructions/s
-VALU_PEAK_GINSTS = 256 * 4 * 2.4 / 4
+FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 vector spec
+PROFILE_ROUND = "r03"
+PROF = ROOT / "profiles"
+TRAFFIC_FILE = PROF / f"{PROFILE_ROUND}_fet_traffic.json"
+VALU_FILE = PROF / f"{PROFILE_ROUND}_fet_valu.json"
+CSS_VALU_FILE = PROF / f"{PROFILE_ROUND}_css_valu.json"
+UBENCH_FILE = PROF / f"{PROFILE_ROUND}_ubench_valu.json"
+
+
+def valu_peak():
+    """VALU issue peak in G wave-instructions/s: the measured simple-integer/FP32 issue rate
+    of tools/ubench_valu.hip (profiles/<R>_ubench_valu.json) when committed, else the
+    MI355X_MICROARCH.md figure (a wave64 instruction over 2 cycles on a SIMD-32 once two or
+    more waves share it: 256 CUs x 4 SIMDs x 2.4 GHz / 2)."""
+    if UBENCH_FILE.exists():
+        u = json.loads(UBENCH_FILE.read_text())
+        return float(u["peak_ginsts"]), f"{UBENCH_FILE.relative_to(ROOT)} ({u['method']})"
+    return 256 * 4 * 2.4 / 2, "MI355X_MICROARCH.md (2 cycles per wave64 VALU instruction per SIMD)"
 
 
 def parse():
@@ -66,115 +82,76 @@ def parse():
     ap.add_argument("--wsize", type=int, default=2500)
     ap.add_argument("--wstep", type=int, default=500)
     ap.add_argument("--perc", type=float, default=0.95)
-    ap.add_argument("--cpu-chroms", type=int, default=20, help="chromosomes in the CPU-baseline sample")
+    ap.add_argument("--cpu-chroms", type=int, default=20, help="chromosomes in the FET CPU-baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--no-css", action="store_true", help="skip the CSS leg")
+    ap.add_argument("--no-css", action="store_true", help="skip the CSS legs")
+    ap.add_argument("--no-c45", action="store_true", help="skip the C4/C5 CSS legs")
     ap.add_argument("--no-extra", action="store_true", help="skip the region-filter and packed-track legs")
     ap.add_argument("--css-steps", type=int, default=3)
-    ap.add_argument("--css-cpu-snps", type=int, default=150_000, help="SNPs in the CSS CPU-baseline sample")
+    ap.add_argument("--c45-chroms", type=int, default=25, help="C4/C5 chromosomes per GPU (configs[3]/[4]: 200/8)")
+    ap.add_argument("--c45-steps", type=int, default=2)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target wall time of each CSS CPU sample")
+    ap.add_argument("--backend", default="nccl")
+    ap.add_argument("--dry-run", action="store_true", help="distributed plumbing only, no GPU work (CPU tests)")
     return ap.parse_args()
 
 
-def css_cpu_baseline(args):
-    """The CSS oracle port (1 thread) on a prefix of chromosome 0 of the same workload."""
-    from gdscan import synth
-    orc = ROOT / "oracle" / "_build" / "liboracle.so"
-    DP = np.ctypeslib.ndpointer(np.float64, flags="C")
-    IP = np.ctypeslib.ndpointer(np.int32, flags="C")
-    C = ctypes
-    lib = C.CDLL(str(orc))
-    fn = lib.orc_css_scan
-    fn.argtypes = [DP, DP, IP, IP, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_uint64,
-                   C.c_int, DP, DP]
-    av, bv, ap_, bp, regend = synth.chromosome(0, args.css_cpu_snps, args.asize, args.bsize)
-    n = regend // args.wstep
-    s, p = np.zeros(n), np.zeros(n)
-    t0 = time.perf_counter()
-    fn(av, bv, ap_, bp, regend, args.wsize, args.wstep, len(av), len(bv), 10, 0, 1, 0, s, p)
-    dt = time.perf_counter() - t0
-    from gdscan import fet
-    w = fet.window_count(regend, args.wsize, args.wstep)
-    return {"value": w / dt, "unit": "windows/s", "cores": 1, "kind": "port",
-            "sample": f"chromosome 0 prefix, {args.css_cpu_snps} SNPs ({args.asize}+{args.bsize}), {w} windows "
-                      f"in {dt:.2f} s, 1 thread (cyclic-Jacobi restatement; the reference CSS needs GSL, "
-                      f"absent here)"}
+def maybe_launch(args):
+    """--gpus N > 1 without a launcher: run torch.distributed.run as a child (no GPU call
+    has happened yet in this process) and return its exit code; None when already a rank."""
+    if args.gpus <= 1 or "WORLD_SIZE" in os.environ:
+        return None
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", str(Path(__file__).resolve())] + sys.argv[1:]
+    return subprocess.call(cmd)
 
 
-def css_shape_run(args, lib, _lib, synth, Chrom, check, dev, stream, ctx, rank, nchrom, pop, treshold, runs):
-    """One timed CSS scan of `nchrom` synthetic chromosomes with pop+pop individuals."""
-    import torch
-    nsnp = args.nsnp
-    alen = nsnp * pop
-    av = torch.empty(nchrom * alen, dtype=torch.float64, device=dev)
-    bv = torch.empty(nchrom * alen, dtype=torch.float64, device=dev)
-    ap = torch.empty(nchrom * alen, dtype=torch.int32, device=dev)
-    bp = torch.empty(nchrom * alen, dtype=torch.int32, device=dev)
-    qtab = torch.from_numpy(synth.freq_table()).to(dev)
-    for c in range(nchrom):
-        check(lib.gd_synth_device(1000 + rank * nchrom + c, nsnp, pop, pop, synth.MASTER_SEED, qtab.data_ptr(),
-                                  av.data_ptr() + c * alen * 8, bv.data_ptr() + c * alen * 8,
-                                  ap.data_ptr() + c * alen * 4, bp.data_ptr() + c * alen * 4, stream))
-    torch.cuda.synchronize()
-    last = ap.view(nchrom, alen)[:, -1].cpu().numpy().astype(np.int64)
-    chroms = (Chrom * nchrom)()
-    w_out = windows = 0
-    for c in range(nchrom):
-        regend = int(last[c]) + 1
-        chroms[c].a_off = chroms[c].b_off = c * alen
-        chroms[c].alen = chroms[c].blen = alen
-        chroms[c].regend = regend
-        chroms[c].w_out = w_out
-        chroms[c].seed = synth.MASTER_SEED + 1000 + c
-        w_out += regend // args.wstep
-        windows += lib.gd_window_count(regend, args.wsize, args.wstep, _lib.GD_WINDOWS_THREADED)
-    sc = torch.zeros(w_out, dtype=torch.float64, device=dev)
-    pv = torch.zeros_like(sc)
-
-    def step():
-        check(lib.gd_css_scan_device(ctx, chroms, nchrom, av.data_ptr(), bv.data_ptr(), ap.data_ptr(), bp.data_ptr(),
-                                     args.wsize, args.wstep, treshold, runs, _lib.GD_WINDOWS_THREADED,
-                                     sc.data_ptr(), pv.data_ptr(), stream))
-
-    step()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    step()
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
-    stage = _lib.last_stage_ms()  # the timed step's HIP events: [1] planes + MDS, [2] permutations
-    pm = pv.cpu().numpy()
-    computed = sc.cpu().numpy() != 0
-    out = {"value": windows / dt, "unit": "windows/s (one GPU)", "ms": dt * 1e3, "windows": windows,
-           "config": f"{nchrom} chromosomes x {nsnp} SNPs, {pop}+{pop}, mcT={treshold}, mcR={runs}",
-           "mean_p": float(pm[computed].mean()) if computed.any() else None,
-           "stage_ms": {"planes_mds": stage[1], "permutations": stage[2]}}
-    if runs > 0 and computed.any():
-        # permutations run per window, from p = (hits + 1) / (run + 1): an early exit (hits =
-        # mcT) leaves p > mcT / (mcR + 1), a full run p <= mcT / (mcR + 1)
-        p = pm[computed]
-        early = p * (runs + 1) > treshold + 0.5
-        nrun = np.where(early, np.rint((treshold + 1) / p) - 1, runs)
-        perms = float(nrun.sum())
-        # SURVEY.md 8(d): (a*b + a + b) FP64 adds per permutation actually run
-        ach = perms * (pop * pop + 2 * pop) / (stage[2] * 1e-3) / 1e12
-        out["permutations"] = {
-            "total": perms, "mean_per_window": float(nrun.mean()),
-            "histogram": {"<=10": int((nrun <= 10).sum()), "11-100": int(((nrun > 10) & (nrun <= 100)).sum()),
-                          f"101-{runs - 1}": int(((nrun > 100) & (nrun < runs)).sum()),
-                          str(runs): int((nrun >= runs).sum())},
-            "per_s": perms / (stage[2] * 1e-3),
-            # the adds run as FP32 pre-filter gathers (FP64 only near ties); the kernel is bound
-            # by LDS gathers and their latency, the FLOP figure is the survey's normalisation
-            "roofline": {"bound": "LDS / latency", "achieved": ach, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": ach / FP64_PEAK_TFLOPS, "kernel": "k_css_perm (HIP events)",
-                         "kernel_ms": stage[2]}}
-    return out
+def host_cpus():
+    """(usable cores, nproc, CPU model): the affinity set, capped by a cgroup CPU quota and by
+    OMP_NUM_THREADS when the box sets it (the GPU box's CPU share; nproc shows the machine)."""
+    usable = len(os.sched_getaffinity(0))
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            usable = min(usable, max(1, int(int(q) / int(per))))
+    except (OSError, ValueError):
+        pass
+    if os.environ.get("OMP_NUM_THREADS", "").isdigit():
+        usable = min(usable, int(os.environ["OMP_NUM_THREADS"]))
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return usable, os.cpu_count(), model
 
 
-def cpu_baseline(args):
-    """Reference threadcompute() (64 pthreads) on a sample of the same workload."""
-    from gdscan import synth
+# ----------------------------------------------------------------------------- CPU baselines
+def silenced(fn):
+    """Run fn() with C stdout sent to /dev/null (the reference prints progress)."""
+    sys.stdout.flush()
+    saved = os.dup(1)
+    devnull = os.open(os.devnull, os.O_WRONLY)
+    os.dup2(devnull, 1)
+    try:
+        return fn()
+    finally:
+        os.dup2(saved, 1)
+        os.close(saved)
+        os.close(devnull)
 
+
+def fet_cpu_baseline(args, scores_dev, chroms):
+    """The reference's threadcompute() (64 pthreads) on the same chromosomes; its scores
+    (seed-independent) are compared with the GPU scores of the same windows."""
+    from gdscan import fet, synth
     ref = ROOT / "oracle" / "_ref" / "libref_fisher.so"
     orc = ROOT / "oracle" / "_build" / "liboracle.so"
     DP = np.ctypeslib.ndpointer(np.float64, flags="C")
@@ -184,49 +161,101 @@ def cpu_baseline(args):
         lib = C.CDLL(str(ref))
         fn = lib.threadcompute
         fn.argtypes = [DP, DP, IP, IP] + [C.c_int] * 6 + [C.c_double, DP, DP]
-        kind, cores = "reference", 64
+        kind = "reference"
     else:
         lib = C.CDLL(str(orc))
         fn = lib.orc_fet_scan
         fn.argtypes = [DP, DP, IP, IP, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_double, C.c_uint64,
                        C.c_int, DP, DP]
-        kind, cores = "port", 1
+        kind = "port"
+    usable, nproc, model = host_cpus()
+    gpu = scores_dev.cpu().numpy()
     total_w = 0
     total_t = 0.0
+    nwin = exact = 0
+    max_rel = 0.0
     for c in range(args.cpu_chroms):
         av, bv, ap_, bp, regend = synth.chromosome(c, args.nsnp, args.asize, args.bsize)
         n = regend // args.wstep
-        s = np.zeros(n)
-        d = np.zeros(n)
-        # the reference prints progress on C stdout: silence it around the call
-        sys.stdout.flush()
-        saved = os.dup(1)
-        devnull = os.open(os.devnull, os.O_WRONLY)
-        os.dup2(devnull, 1)
-        try:
+        s, d = np.zeros(n), np.zeros(n)
+
+        def call():
             t0 = time.perf_counter()
             if kind == "reference":
                 fn(av, bv, ap_, bp, 0, regend, args.wsize, args.wstep, len(av), len(bv), args.perc, s, d)
             else:
                 fn(av, bv, ap_, bp, regend, args.wsize, args.wstep, len(av), len(bv), args.perc, 1, 0, s, d)
-            total_t += time.perf_counter() - t0
-        finally:
-            os.dup2(saved, 1)
-            os.close(saved)
-            os.close(devnull)
-        from gdscan import fet
+            return time.perf_counter() - t0
+
+        total_t += silenced(call)
         total_w += fet.window_count(regend, args.wsize, args.wstep)
+        g = gpu[chroms[c].w_out:chroms[c].w_out + n]
+        comp = (s != 0) | (g != 0)
+        nwin += int(comp.sum())
+        exact += int((s[comp] == g[comp]).sum())
+        rel = np.abs(s[comp] - g[comp]) / np.maximum(np.abs(s[comp]), 1e-300)
+        max_rel = max(max_rel, float(rel.max()) if rel.size else 0.0)
+    threads = 64 if kind == "reference" else 1
     return {
-        "value": total_w / total_t,
-        "unit": "windows/s",
-        "cores": cores,
-        "kind": kind,
-        "sample": f"{args.cpu_chroms} of the {args.nchrom} chromosomes ({args.nsnp} SNPs, "
-                  f"{args.asize}+{args.bsize}), {total_w} windows in {total_t:.2f} s"
-                  + (" with the reference's 64 pthreads" if kind == "reference" else ", 1 thread"),
+        "value": total_w / total_t, "unit": "windows/s", "cores": min(threads, usable), "kind": kind,
+        "threads": threads, "nproc": nproc, "cpu_model": model,
+        "sample": f"{args.cpu_chroms} of the {args.nchrom} chromosomes ({args.nsnp} SNPs, {args.asize}+{args.bsize}), "
+                  f"{total_w} windows in {total_t:.2f} s"
+                  + (f" with the reference's 64 pthreads on {min(64, usable)} usable cores" if kind == "reference"
+                     else ", 1 thread"),
+        "parity": {"windows": nwin, "bit_exact_frac": exact / max(nwin, 1), "max_rel": max_rel,
+                   "what": "reference threadcompute scores vs the GPU scores of the same windows (scores are "
+                           "seed-independent; stddev is time-seeded in the reference)"},
     }
 
 
+def css_cpu_baseline(args, pop, treshold, runs):
+    """The CSS oracle port (the reference CSS needs GSL, absent here) threaded over the host's
+    usable cores: one chromosome prefix per thread (ctypes releases the GIL), each sized from
+    a short calibration so the sample takes about --cpu-seconds of wall time."""
+    from concurrent.futures import ThreadPoolExecutor
+    from gdscan import fet, synth
+    usable, nproc, model = host_cpus()
+    threads = max(1, min(usable, 64))
+    orc = ROOT / "oracle" / "_build" / "liboracle.so"
+    DP = np.ctypeslib.ndpointer(np.float64, flags="C")
+    IP = np.ctypeslib.ndpointer(np.int32, flags="C")
+    C = ctypes
+    lib = C.CDLL(str(orc))
+    fn = lib.orc_css_scan
+    fn.argtypes = [DP, DP, IP, IP, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_uint64,
+                   C.c_int, DP, DP]
+
+    def data(c, nsnp):
+        av, bv, ap_, bp, regend = synth.chromosome(5000 + c, nsnp, pop, pop)
+        n = regend // args.wstep
+        return av, bv, ap_, bp, regend, np.zeros(n), np.zeros(n)
+
+    def run(c, d):
+        av, bv, ap_, bp, regend, s, p = d
+        t0 = time.perf_counter()
+        fn(av, bv, ap_, bp, regend, args.wsize, args.wstep, len(av), len(bv), treshold, runs, 1 + c, 0, s, p)
+        return time.perf_counter() - t0, fet.window_count(regend, args.wsize, args.wstep)
+
+    # calibration: one thread, a prefix long enough for the threaded window set (>= 103 steps)
+    dt, w = run(0, data(0, 6_000))
+    per_w = dt / max(w, 1)
+    # ~10 new SNPs per 500-bp window step (mean gap 50 bp): SNPs for --cpu-seconds per thread
+    nsnp = int(min(500_000, max(6_000, 10.0 * args.cpu_seconds / max(per_w, 1e-9))))
+    inputs = [data(c, nsnp) for c in range(threads)]
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(threads) as ex:
+        res = list(ex.map(lambda c: run(c, inputs[c]), range(threads)))
+    wall = time.perf_counter() - t0
+    win = sum(r[1] for r in res)
+    return {"value": win / wall, "unit": "windows/s", "cores": threads, "kind": "port", "nproc": nproc,
+            "cpu_model": model,
+            "sample": f"{threads} chromosome prefixes of {nsnp} SNPs ({pop}+{pop}, mcT={treshold}, mcR={runs}), one "
+                      f"per thread, {win} windows in {wall:.2f} s (oracle/css_oracle.c, cyclic-Jacobi restatement; "
+                      f"the reference CSS needs GSL, absent here)"}
+
+
+# ----------------------------------------------------------------------------- FET extras
 def regions_run(args, scores, stddev, chroms, nch, rank, world, dev):
     """FilterFisherScores on the FET track just computed, kept in HBM:
     the tabular track (windows with score != 0), its limit (cmedian + scoreatpercentile)
@@ -332,8 +361,6 @@ def host_run(args, lib, _lib, check, avals, bvals, apos, bpos, chroms, nch, scor
     (gd_fet_scan_host_batch: f64 value + i32 position per genotype; gd_fet_scan_packed_host:
     2-bit codes + one position per row).  A sample of the rank's chromosomes; reported
     beside the headline, never as `value`."""
-    import numpy as np
-    import torch
     from gdscan._lib import Chrom
     a, b, nsnp = args.asize, args.bsize, args.nsnp
     nh = min(nch, 4)
@@ -364,7 +391,7 @@ def host_run(args, lib, _lib, check, avals, bvals, apos, bpos, chroms, nch, scor
             best = dt if best is None or dt < best else best
         return best, s_, d_
 
-    import ctypes as C
+    C = ctypes
     pd_ = lambda x: x.ctypes.data_as(C.POINTER(C.c_double))
     pi_ = lambda x: x.ctypes.data_as(C.POINTER(C.c_int))
     pv_ = lambda x: x.ctypes.data
@@ -386,24 +413,320 @@ def host_run(args, lib, _lib, check, avals, bvals, apos, bpos, chroms, nch, scor
                            and np.array_equal(s2, ref_s) and np.array_equal(d2, ref_d))}
 
 
+# ----------------------------------------------------------------------------- CSS legs
+class Env:
+    """What every leg needs: the library, this rank's device, stream, context, process group."""
+
+    def __init__(self, args, rank, world, local, dist):
+        import torch
+        from gdscan import _lib, synth
+        from gdscan._lib import Chrom, check, lib
+        self.args, self.rank, self.world, self.dist = args, rank, world, dist
+        self.torch, self._lib, self.synth, self.Chrom, self.check, self.lib = torch, _lib, synth, Chrom, check, lib
+        self.dev = torch.device("cuda", local)
+        self.stream = torch.cuda.current_stream(self.dev).cuda_stream
+        self.ctx = lib.gd_ctx_create(local)
+        assert self.ctx, "gd_ctx_create failed"
+
+    def max_over_ranks(self, x):
+        if not self.dist:
+            return x
+        t = self.torch.tensor([x], dtype=self.torch.float64, device=self.dev)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def sync(self):
+        self.torch.cuda.synchronize()
+        if self.dist:
+            self.dist.barrier()
+        self.torch.cuda.synchronize()
+
+
+def css_valu(shape_key, windows, kernel_ms):
+    """VALU-issue figure of a CSS leg from the committed PMC profile (wave-instructions per
+    window of the kernels the leg dispatches), over this run's kernel time."""
+    if not CSS_VALU_FILE.exists():
+        return None
+    doc = json.loads(CSS_VALU_FILE.read_text()).get(shape_key)
+    if not doc or kernel_ms <= 0:
+        return None
+    peak, src = valu_peak()
+    gi = doc["valu_wave_insts_per_window"] * windows / (kernel_ms * 1e-3) / 1e9
+    return {"bound": "valu-issue", "achieved": gi, "peak": peak, "unit": "G wave-insts/s", "frac": gi / peak,
+            "insts_per_window": doc["valu_wave_insts_per_window"], "kernels": doc["kernels"],
+            "source": f"{CSS_VALU_FILE.relative_to(ROOT)} [{shape_key}] ({doc['method']}); peak: {src}"}
+
+
+def perm_stats(pm, computed, treshold, runs, perm_ms, pop):
+    """Permutations actually run per window, from p = (hits + 1) / (run + 1): an early exit
+    (hits = mcT) leaves p > mcT / (mcR + 1), a full run p <= mcT / (mcR + 1)."""
+    p = pm[computed]
+    early = p * (runs + 1) > treshold + 0.5
+    nrun = np.where(early, np.rint((treshold + 1) / p) - 1, runs)
+    perms = float(nrun.sum())
+    # SURVEY.md 8(d): (a*b + a + b) FP64 adds per permutation actually run
+    ach = perms * (pop * pop + 2 * pop) / (perm_ms * 1e-3) / 1e12 if perm_ms > 0 else 0.0
+    return {"total": perms, "mean_per_window": float(nrun.mean()),
+            "histogram": {"<=10": int((nrun <= 10).sum()), "11-100": int(((nrun > 10) & (nrun <= 100)).sum()),
+                          f"101-{runs - 1}": int(((nrun > 100) & (nrun < runs)).sum()),
+                          str(runs): int((nrun >= runs).sum())},
+            "per_s": perms / (perm_ms * 1e-3) if perm_ms > 0 else None,
+            # the adds run as FP32 pre-filter gathers (FP64 only near ties): the FLOP figure is
+            # the survey's normalisation, not the kernel's binding resource
+            "roofline": {"bound": "LDS / latency", "achieved": ach, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                         "frac": ach / FP64_PEAK_TFLOPS, "kernel": "k_css_perm (HIP events)", "kernel_ms": perm_ms}}
+
+
+def c3_leg(env, args, chroms, nch, windows, avals, bvals, apos, bpos, scores):
+    """configs[2] shape on the FET leg's resident chromosomes (20+20, runs=0)."""
+    torch, lib, _lib, check = env.torch, env.lib, env._lib, env.check
+    pv = torch.zeros_like(scores)
+
+    def step():
+        check(lib.gd_css_scan_device(env.ctx, chroms, nch, avals.data_ptr(), bvals.data_ptr(), apos.data_ptr(),
+                                     bpos.data_ptr(), args.wsize, args.wstep, 10, 0, _lib.GD_WINDOWS_THREADED,
+                                     scores.data_ptr(), pv.data_ptr(), env.stream))
+
+    step()
+    env.sync()
+    t0 = time.perf_counter()
+    kms = 0.0
+    for _ in range(args.css_steps):
+        step()
+        kms += _lib.last_stage_ms()[1]  # bit planes -> scores (HIP events)
+    env.sync()
+    el = env.max_over_ranks(time.perf_counter() - t0)
+    kms /= args.css_steps
+    m = args.asize + args.bsize
+    flops = (4.0 / 3.0 * m ** 3 + 10.0 * m * m) * windows
+    ach = flops / (kms * 1e-3) / 1e12
+    out = {"metric": "CSS genomic windows/sec (classical MDS, runs=0; per-GPU batch)",
+           "value": windows * env.world * args.css_steps / el, "unit": "windows/s",
+           "ms_per_step": el * 1e3 / args.css_steps, "steps": args.css_steps,
+           "config": {"workload": f"CSS, configs[2] shape: {nch} chromosomes x {args.nsnp} SNPs per GPU, "
+                                  f"{args.asize}+{args.bsize} individuals, wsize {args.wsize}, wstep {args.wstep}, mcR=0",
+                      "windows_per_gpu": windows},
+           "roofline": {"bound": "fp64-valu", "achieved": ach, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                        "frac": ach / FP64_PEAK_TFLOPS, "traffic": None,
+                        "kernel": "k_css_pack + k_css_mds_p40 (HIP events)", "kernel_ms": kms,
+                        "alg_flops_per_window": flops / windows}}
+    v = css_valu("c3", windows, kms)
+    if v:
+        out["roofline"]["valu"] = v
+    if env.rank == 0 and env.world == 1 and not args.no_cpu:
+        out["cpu_baseline"] = css_cpu_baseline(args, args.asize, 10, 0)
+    return out
+
+
+def c45_leg(env, args, name, treshold, runs, queue):
+    """configs[3] (runs=0, static shards) / configs[4] (mcR=1000, shared queue) per-GPU share:
+    args.c45_chroms chromosomes x 500k SNPs per GPU at 40+40; the (score, p) track of every
+    rank all-gathered into genome order after the timed steps (timed separately)."""
+    from gdscan.shard import default_store, gather_lists, gather_tracks, plan_shards, queue_pull
+    torch, lib, _lib, check, synth = env.torch, env.lib, env._lib, env.check, env.synth
+    pop, nsnp, world, rank = 40, args.nsnp, env.world, env.rank
+    total = args.c45_chroms * world
+    alen = nsnp * pop
+    shards = plan_shards([nsnp] * total, world)
+    resident = list(range(total)) if queue else shards[rank]
+    nres = len(resident)
+    av = torch.empty(nres * alen, dtype=torch.float64, device=env.dev)
+    bv = torch.empty(nres * alen, dtype=torch.float64, device=env.dev)
+    ap = torch.empty(nres * alen, dtype=torch.int32, device=env.dev)
+    bp = torch.empty(nres * alen, dtype=torch.int32, device=env.dev)
+    qtab = torch.from_numpy(synth.freq_table()).to(env.dev)
+    for i, c in enumerate(resident):
+        check(lib.gd_synth_device(1000 + c, nsnp, pop, pop, synth.MASTER_SEED, qtab.data_ptr(),
+                                  av.data_ptr() + i * alen * 8, bv.data_ptr() + i * alen * 8,
+                                  ap.data_ptr() + i * alen * 4, bp.data_ptr() + i * alen * 4, env.stream))
+    torch.cuda.synchronize()
+    last = ap.view(nres, alen)[:, -1].cpu().numpy().astype(np.int64)
+    reg_local = {c: int(last[i]) + 1 for i, c in enumerate(resident)}
+    if queue:
+        regends = [reg_local[c] for c in range(total)]
+    else:
+        got = gather_lists([reg_local[c] for c in resident]) if env.dist else [[reg_local[c] for c in resident]]
+        regends = [0] * total
+        for r, s in enumerate(shards):
+            for c, v in zip(s, got[r]):
+                regends[c] = v
+    wins = [g // args.wstep for g in regends]
+    wcount = [lib.gd_window_count(g, args.wsize, args.wstep, _lib.GD_WINDOWS_THREADED) for g in regends]
+    # descriptors of the resident chromosomes; queue: outputs at genome offsets, static: the
+    # rank's shard concatenated (gather_tracks' local layout)
+    gofs = np.concatenate([[0], np.cumsum(wins)]).astype(np.int64)
+    chroms = (env.Chrom * nres)()
+    w = 0
+    for i, c in enumerate(resident):
+        d = chroms[i]
+        d.a_off = d.b_off = i * alen
+        d.alen = d.blen = alen
+        d.regend = regends[c]
+        d.w_out = int(gofs[c]) if queue else w
+        d.seed = synth.MASTER_SEED + 1000 + c
+        w += wins[c]
+    nout = int(gofs[-1]) if queue else w
+    sc = torch.zeros(max(nout, 1), dtype=torch.float64, device=env.dev)
+    pv = torch.zeros_like(sc)
+    stage = np.zeros(2)
+    my_windows = sum(wcount[c] for c in resident) if not queue else 0
+
+    def scan(idx, n):
+        ptr = ctypes.cast(ctypes.addressof(chroms) + idx * ctypes.sizeof(env.Chrom), ctypes.POINTER(env.Chrom))
+        check(lib.gd_css_scan_device(env.ctx, ptr, n, av.data_ptr(),
+                                     bv.data_ptr(), ap.data_ptr(), bp.data_ptr(), args.wsize, args.wstep, treshold,
+                                     runs, _lib.GD_WINDOWS_THREADED, sc.data_ptr(), pv.data_ptr(), env.stream))
+        st = _lib.last_stage_ms()
+        stage[0] += st[1]
+        stage[1] += st[2]
+
+    store = default_store() if (queue and env.dist) else None
+    tick = [0]
+
+    def step(k):
+        if not queue:
+            scan(0, nres)
+            return list(resident)
+        if store is None:  # one rank: the queue is the chromosome order
+            for c in range(total):
+                scan(c, 1)
+            return list(range(total))
+        done = queue_pull(store, f"gd_{name}_{k}", total, lambda c: scan(c, 1))
+        return done
+
+    step(-1)  # warmup (sizes the workspace)
+    env.sync()
+    stage[:] = 0
+    busy = []
+    done = []
+    t0 = time.perf_counter()
+    for k in range(args.c45_steps):
+        b0 = time.perf_counter()
+        done = step(k)
+        busy.append(time.perf_counter() - b0)
+    env.sync()
+    el = env.max_over_ranks(time.perf_counter() - t0)
+    stage /= args.c45_steps
+    all_windows = sum(wcount)
+    out = {"metric": f"CSS genomic windows/sec ({'configs[4]: mcT=10, mcR=1000' if runs else 'configs[3]: runs=0'}; "
+                     f"{args.c45_chroms} chromosomes per GPU)",
+           "value": all_windows * args.c45_steps / el, "unit": "windows/s", "n_gpus": world,
+           "ms_per_step": el * 1e3 / args.c45_steps, "steps": args.c45_steps,
+           "config": {"workload": f"{total} chromosomes x {nsnp} SNPs ({args.c45_chroms} per GPU), 40+40, "
+                                  f"wsize {args.wsize}, wstep {args.wstep}, mcT={treshold}, mcR={runs}",
+                      "windows": all_windows,
+                      "sharding": "shared chromosome queue (store counter), inputs resident on every rank"
+                      if queue else "plan_shards (LPT by SNP count), whole chromosomes per rank"}}
+    # the one collective: (score, p) of every rank's chromosomes, all-gathered in genome order
+    if env.dist:
+        shard_done = gather_lists(done) if queue else shards
+        mine = shard_done[rank]
+        if queue:
+            local = torch.cat([torch.stack([sc[gofs[c]:gofs[c + 1]], pv[gofs[c]:gofs[c + 1]]], 1) for c in mine]) \
+                if mine else torch.zeros((0, 2), dtype=torch.float64, device=env.dev)
+        else:
+            local = torch.stack([sc[:nout], pv[:nout]], 1)
+        env.sync()
+        g0 = time.perf_counter()
+        track = gather_tracks(local, shard_done, wins)
+        torch.cuda.synchronize()
+        out["track_gather_ms"] = env.max_over_ranks((time.perf_counter() - g0) * 1e3)
+        sc_all, p_all = track[:, 0], track[:, 1]
+        busy_all = gather_lists([int(1e6 * sum(busy))])
+        per_rank = [b[0] * 1e-6 for b in busy_all]
+        out["per_rank_busy_s"] = per_rank
+        out["imbalance"] = max(per_rank) / (sum(per_rank) / len(per_rank))
+        if queue:
+            out["chromosomes_per_rank"] = [len(s) for s in shard_done]
+    else:
+        sc_all, p_all = sc[:nout], pv[:nout]
+        out["track_gather_ms"] = None
+    pm, sm = p_all.cpu().numpy(), sc_all.cpu().numpy()
+    computed = sm != 0
+    m = 2 * pop
+    flops = (4.0 / 3.0 * m ** 3 + 10.0 * m * m)
+    # per-rank kernel time of the MDS stage over the windows this rank scanned
+    mine_w = sum(wcount[c] for c in done) if queue else my_windows
+    ach = flops * mine_w / (stage[0] * 1e-3) / 1e12 if stage[0] > 0 else 0.0
+    out["roofline"] = {"bound": "fp64-valu", "achieved": ach, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                       "frac": ach / FP64_PEAK_TFLOPS, "kernel": "k_css_pack + k_css_mds_t80 (HIP events, rank 0)",
+                       "kernel_ms": float(stage[0]), "alg_flops_per_window": flops}
+    v = css_valu("c4", mine_w, float(stage[0]))
+    if v:
+        out["roofline"]["valu"] = v
+    out["stage_ms"] = {"planes_mds": float(stage[0]), "permutations": float(stage[1])}
+    out["mean_p"] = float(pm[computed].mean()) if computed.any() else None
+    if runs > 0 and computed.any():
+        perm_ms = float(stage[1])
+        if env.dist:  # GPU-time of the permutation kernel summed over ranks
+            t = torch.tensor([perm_ms], dtype=torch.float64, device=env.dev)
+            env.dist.all_reduce(t)
+            perm_ms = float(t.item())
+        out["permutations"] = perm_stats(pm, computed, treshold, runs, perm_ms, pop)
+        pv_ = css_valu("c5_perm", mine_w, float(stage[1]))
+        if pv_:
+            out["permutations"]["valu"] = pv_
+    if env.rank == 0 and env.world == 1 and not args.no_cpu:
+        out["cpu_baseline"] = css_cpu_baseline(args, pop, treshold, runs)
+    del av, bv, ap, bp
+    return out
+
+
+# ----------------------------------------------------------------------------- dry run (CPU)
+def dry_run(args, rank, world, dist):
+    """The distributed plumbing without a GPU: shard plan, the chromosome queue over the
+    default store, and the track gather (gloo), checked against the expected genome order."""
+    import torch
+    from gdscan.shard import default_store, gather_lists, gather_tracks, plan_shards, queue_pull
+    total = args.c45_chroms * world
+    wins = [100 + 7 * c for c in range(total)]
+    offs = np.concatenate([[0], np.cumsum(wins)])
+    store = default_store()
+    done = queue_pull(store, "gd_dry", total, lambda c: time.sleep(0.001 * (1 + c % 3)))
+    lists = gather_lists(done)
+    assert sorted(c for s in lists for c in s) == list(range(total))
+    local = torch.cat([torch.stack([torch.arange(offs[c], offs[c + 1], dtype=torch.float64)] * 2, 1) for c in done]) \
+        if done else torch.zeros((0, 2), dtype=torch.float64)
+    track = gather_tracks(local, lists, wins)
+    ok = bool(torch.equal(track[:, 0], torch.arange(offs[-1], dtype=torch.float64)))
+    shards = plan_shards([args.nsnp] * total, world)
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "n_gpus": world, "backend": args.backend, "queue_per_rank":
+                          [len(s) for s in lists], "static_per_rank": [len(s) for s in shards], "gather_ok": ok}),
+              flush=True)
+    dist.barrier()
+
+
+# ----------------------------------------------------------------------------- main
 def main():
     args = parse()
+    rc = maybe_launch(args)
+    if rc is not None:
+        sys.exit(rc)
     import torch
 
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))
-    torch.cuda.set_device(local)
     dist = None
+    if args.dry_run:
+        import torch.distributed as dist_mod
+        if world > 1:
+            dist_mod.init_process_group(args.backend)
+            dry_run(args, rank, world, dist_mod)
+            dist_mod.destroy_process_group()
+        else:
+            print(json.dumps({"dry_run": True, "n_gpus": 1}), flush=True)
+        return
+    torch.cuda.set_device(local)
     if world > 1:
         import torch.distributed as dist_mod
-        dist_mod.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dist_mod.init_process_group(args.backend, device_id=torch.device("cuda", local))
         dist = dist_mod
 
-    from gdscan import _lib, synth
-    from gdscan._lib import Chrom, check, lib
-
-    dev = torch.device("cuda", local)
+    env = Env(args, rank, world, local, dist)
+    lib, _lib, synth, check = env.lib, env._lib, env.synth, env.check
+    dev, stream, ctx = env.dev, env.stream, env.ctx
     a, b, nsnp, nch = args.asize, args.bsize, args.nsnp, args.nchrom
     alen, blen = nsnp * a, nsnp * b
     avals = torch.empty(nch * alen, dtype=torch.float64, device=dev)
@@ -411,7 +734,6 @@ def main():
     apos = torch.empty(nch * alen, dtype=torch.int32, device=dev)
     bpos = torch.empty(nch * blen, dtype=torch.int32, device=dev)
     qtab = torch.from_numpy(synth.freq_table()).to(dev)
-    stream = torch.cuda.current_stream(dev).cuda_stream
     for c in range(nch):
         gc = rank * nch + c
         check(lib.gd_synth_device(gc, nsnp, a, b, synth.MASTER_SEED, qtab.data_ptr(),
@@ -420,7 +742,7 @@ def main():
     torch.cuda.synchronize()
     # regend of each chromosome = last position + 1
     last = apos.view(nch, alen)[:, -1].cpu().numpy().astype(np.int64)
-    chroms = (Chrom * nch)()
+    chroms = (env.Chrom * nch)()
     w_out = 0
     windows = 0
     for c in range(nch):
@@ -436,8 +758,6 @@ def main():
         windows += lib.gd_window_count(regend, args.wsize, args.wstep, _lib.GD_WINDOWS_THREADED)
     scores = torch.zeros(w_out, dtype=torch.float64, device=dev)
     stddev = torch.zeros(w_out, dtype=torch.float64, device=dev)
-    ctx = lib.gd_ctx_create(local)
-    assert ctx, "gd_ctx_create failed"
 
     def step():
         check(lib.gd_fet_scan_device(ctx, chroms, nch, avals.data_ptr(), bvals.data_ptr(), apos.data_ptr(),
@@ -447,21 +767,13 @@ def main():
     for _ in range(args.warmup):
         step()
     stage = np.zeros(_lib.GD_NSTAGES)
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
+    env.sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
         stage += np.array(_lib.last_stage_ms())
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    env.sync()
+    elapsed = env.max_over_ranks(time.perf_counter() - t0)
     stage /= args.steps
     ms_per_step = elapsed * 1e3 / args.steps
     gather_ms = None
@@ -473,12 +785,12 @@ def main():
         wt[rank * nch:(rank + 1) * nch] = torch.tensor([chroms[c].regend // args.wstep for c in range(nch)])
         dist.all_reduce(wt)  # every rank learns every chromosome's window count
         shards = [list(range(r * nch, (r + 1) * nch)) for r in range(world)]
-        local = torch.stack([scores, stddev], 1)
-        torch.cuda.synchronize()
+        loc = torch.stack([scores, stddev], 1)
+        env.sync()
         g0 = time.perf_counter()
-        gather_tracks(local, shards, wt.tolist())
+        gather_tracks(loc, shards, wt.tolist())
         torch.cuda.synchronize()
-        gather_ms = (time.perf_counter() - g0) * 1e3
+        gather_ms = env.max_over_ranks((time.perf_counter() - g0) * 1e3)
     total_windows = windows * world
     value = total_windows * args.steps / elapsed
 
@@ -512,8 +824,8 @@ def main():
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
             "traffic": None,
-            "kernel": "whole scan pipeline (k_popsize, k_bounds, k_snp_fet, k_fet_window_fast; k_fet_lut_* "
-                      "when the score table is cold), HIP events on the scan's streams per step",
+            "kernel": "whole scan pipeline (k_popsize, k_bounds, k_fet_window_fast; k_snp_fet / k_fet_lut_* when "
+                      "the score table is cold), HIP events on the scan's streams per step",
             "alg_bytes_per_step": alg_bytes,
             "stage_ms": {"hbm_passes_done": stage[0], "fast_windows_done": stage[1],
                          "general_path": stage[2], "scan_total": stage[3]},
@@ -525,18 +837,19 @@ def main():
             out["roofline"]["traffic"] = tr["bytes_per_scan"]
             out["roofline"]["traffic_source"] = f"{TRAFFIC_FILE.relative_to(ROOT)} ({tr['method']})"
     if VALU_FILE.exists():
-        # the binding resource of the scan: VALU issue (the bootstrap's nrand48 draws),
-        # not HBM -- wave-instructions per scan (PMC SQ_INSTS_VALU, committed profile)
-        # over this run's scan time, against the VALU issue peak
+        # the binding resource of the scan: VALU issue (the bootstrap's nrand48 draws), not
+        # HBM -- wave-instructions per scan (PMC SQ_INSTS_VALU, committed profile) over this
+        # run's scan time, against the measured VALU issue peak
         vr = json.loads(VALU_FILE.read_text())
         if vr.get("config") == [nch, nsnp, a, b]:
+            peak, src = valu_peak()
             ginst = vr["valu_wave_insts_per_scan"] / (stage[3] * 1e-3) / 1e9
             out["roofline"]["valu"] = {
-                "bound": "valu-issue", "achieved": ginst, "peak": VALU_PEAK_GINSTS, "unit": "G wave-insts/s",
-                "frac": ginst / VALU_PEAK_GINSTS, "insts_per_scan": vr["valu_wave_insts_per_scan"],
-                "source": f"{VALU_FILE.relative_to(ROOT)} ({vr['method']})"}
+                "bound": "valu-issue", "achieved": ginst, "peak": peak, "unit": "G wave-insts/s",
+                "frac": ginst / peak, "insts_per_scan": vr["valu_wave_insts_per_scan"],
+                "source": f"{VALU_FILE.relative_to(ROOT)} ({vr['method']}); peak: {src}"}
     if rank == 0 and world == 1 and not args.no_cpu:
-        out["cpu_baseline"] = cpu_baseline(args)
+        out["cpu_baseline"] = fet_cpu_baseline(args, scores, chroms)
 
     if not args.no_extra:
         out["regions"] = regions_run(args, scores, stddev, chroms, nch, rank, world, dev)
@@ -548,72 +861,18 @@ def main():
         del codes
 
     if not args.no_css:
-        pv = torch.zeros_like(scores)
-
-        def css_step():
-            check(lib.gd_css_scan_device(ctx, chroms, nch, avals.data_ptr(), bvals.data_ptr(), apos.data_ptr(),
-                                         bpos.data_ptr(), args.wsize, args.wstep, 10, 0, _lib.GD_WINDOWS_THREADED,
-                                         scores.data_ptr(), pv.data_ptr(), stream))
-
-        css_step()
-        if dist:
-            dist.barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        kms = 0.0
-        for _ in range(args.css_steps):
-            css_step()
-            kms += _lib.last_stage_ms()[1]  # the CSS window kernel (bit planes -> scores)
-        torch.cuda.synchronize()
-        if dist:
-            dist.barrier()
-        css_elapsed = time.perf_counter() - t0
-        if dist:
-            t = torch.tensor([css_elapsed], dtype=torch.float64, device=dev)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            css_elapsed = float(t.item())
-        kms /= args.css_steps
-        m = a + b
-        flops = (4.0 / 3.0 * m ** 3 + 10.0 * m * m) * windows
-        ach = flops / (kms * 1e-3) / 1e12
-        out["css"] = {
-            "metric": "CSS genomic windows/sec (classical MDS, runs=0; per-GPU batch)",
-            "value": windows * world * args.css_steps / css_elapsed,
-            "unit": "windows/s",
-            "ms_per_step": css_elapsed * 1e3 / args.css_steps,
-            "steps": args.css_steps,
-            "config": {"workload": f"CSS, configs[2] shape: {nch} chromosomes x {nsnp} SNPs per GPU, {a}+{b} "
-                                   f"individuals, wsize {args.wsize}, wstep {args.wstep}, mcR=0",
-                       "windows_per_gpu": windows},
-            "roofline": {"bound": "fp64-valu", "achieved": ach, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": ach / FP64_PEAK_TFLOPS, "traffic": None,
-                         "kernel": "k_css_pack + k_css_mds (HIP events)", "kernel_ms": kms,
-                         "alg_flops_per_window": flops / windows},
-        }
-        if CSS_VALU_FILE.exists():
-            # what binds the MDS kernel: VALU issue -- per-window serial phases (Householder
-            # steps, Sturm bisection, inverse iteration, back-transformation) on a wave whose
-            # lanes hold the matrix rows (40 of 64 busy at m = 40)
-            cv = json.loads(CSS_VALU_FILE.read_text())
-            if cv.get("config") == [nch, nsnp, a, b]:
-                gi = cv["valu_wave_insts_per_scan"] / (kms * 1e-3) / 1e9
-                out["css"]["roofline"]["valu"] = {
-                    "bound": "valu-issue", "achieved": gi, "peak": VALU_PEAK_GINSTS, "unit": "G wave-insts/s",
-                    "frac": gi / VALU_PEAK_GINSTS, "insts_per_window": cv["valu_wave_insts_per_scan"] / windows,
-                    "source": f"{CSS_VALU_FILE.relative_to(ROOT)} ({cv['method']})"}
-        if rank == 0 and world == 1 and not args.no_cpu:
-            out["css"]["cpu_baseline"] = css_cpu_baseline(args)
-        # the per-GPU shapes of configs[3] (40+40, runs=0) and configs[4] (40+40, mcT=10,
-        # mcR=1000) on a few chromosomes of their own: windows/s per GPU
-        del avals, bvals, apos, bpos
-        out["css"]["c4_shape"] = css_shape_run(args, lib, _lib, synth, Chrom, check, dev, stream, ctx, rank,
-                                               nchrom=4, pop=40, treshold=10, runs=0)
-        out["css"]["c5_shape"] = css_shape_run(args, lib, _lib, synth, Chrom, check, dev, stream, ctx, rank,
-                                               nchrom=1, pop=40, treshold=10, runs=1000)
+        out["css"] = c3_leg(env, args, chroms, nch, windows, avals, bvals, apos, bpos, scores)
+        del avals, bvals, apos, bpos, scores, stddev
+        torch.cuda.empty_cache()
+        if not args.no_c45:
+            out["css"]["c4"] = c45_leg(env, args, "c4", 10, 0, queue=False)
+            torch.cuda.empty_cache()
+            out["css"]["c5"] = c45_leg(env, args, "c5", 10, 1000, queue=True)
     lib.gd_ctx_destroy(ctx)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist:
+        dist.barrier()
         dist.destroy_process_group()
 
 

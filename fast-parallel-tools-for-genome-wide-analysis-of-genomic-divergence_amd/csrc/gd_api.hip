@@ -601,7 +601,7 @@ static int host_scan(const double *avals, const double *bvals, const int *apos, 
 static int css_scan_locked(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, const double *avals,
                            const double *bvals, const int32_t *apos, const int32_t *bpos, int wsize, int wstep,
                            int treshold, int runs, int drosophila, int mds, int window_set, double *scores, double *p,
-                           hipStream_t s, const PackedIn *pk = nullptr);
+                           hipStream_t s, const PackedIn *pk = nullptr, double *x_out = nullptr);
 
 /* several chromosomes from host memory in one device scan: H2D of the inputs and of
  * the caller's outputs (kept at uncomputed windows), the batched scan, D2H */
@@ -739,7 +739,7 @@ extern "C" int gd_fet_compute(const double *avals, const double *bvals, const in
 static int css_scan_locked(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, const double *avals,
                            const double *bvals, const int32_t *apos, const int32_t *bpos, int wsize, int wstep,
                            int treshold, int runs, int drosophila, int mds, int window_set, double *scores, double *p,
-                           hipStream_t s, const PackedIn *pk) {
+                           hipStream_t s, const PackedIn *pk, double *x_out) {
   if (drosophila != 0 && drosophila != 1) return fail(GD_ERR_ARG, "drosophila must be 0 or 1");
   if (mds < 0 || mds > 2) return fail(GD_ERR_ARG, "mds must be 0 (classical), 1 (SMACOF) or 2 (SMACOF + classical)");
   if (pk && drosophila)
@@ -871,6 +871,12 @@ static int css_scan_locked(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, cons
                      scores, p, xbuf, status, flags, s, ctx->ev[2]);
   if (st) return fail(st, "CSS kernel launch failed");
   HIP_TRY(hipEventRecord(ctx->ev[3], s));
+  if (x_out && perms) {
+    /* diagnostics (gd_css_coords_host): the coordinates the permutation stage read, one
+     * row of 2 m doubles per window of the batch (xbuf rows are 2 mp wide) */
+    HIP_TRY(hipMemcpy2DAsync(x_out, sizeof(double) * 2 * mmax, xbuf, sizeof(double) * 2 * mp,
+                             sizeof(double) * 2 * mmax, pl.wtotal, hipMemcpyDeviceToHost, s));
+  }
   HIP_TRY(hipMemcpyAsync(ctx->h_flags, flags, 16 * sizeof(unsigned), hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
   float ms;
@@ -913,6 +919,20 @@ extern "C" int gd_css_scan_host_ex(const double *avals, const double *bvals, con
                      ch->seed = seed;
                      return css_scan_locked(ctx, ch, 1, av, bv, ap, bp, wsize, wstep, treshold, runs, drosophila,
                                             mds, window_set, o0, o1, s);
+                   });
+}
+
+extern "C" int gd_css_coords_host(const double *avals, const double *bvals, const int *apos, const int *bpos,
+                                  int regend, int wsize, int wstep, int alen, int blen, int treshold, int runs,
+                                  int mds, uint64_t seed, int window_set, double *scores, double *p, double *X) {
+  if (runs <= 0 || treshold <= 0) return fail(GD_ERR_ARG, "coordinates are kept only for a permutation test");
+  if (!X) return fail(GD_ERR_ARG, "null buffer");
+  return host_scan(avals, bvals, apos, bpos, regend, wsize, wstep, alen, blen, scores, p,
+                   [&](gd_ctx *ctx, gd_chrom *ch, double *av, double *bv, int32_t *ap, int32_t *bp, double *o0,
+                       double *o1, hipStream_t s) {
+                     ch->seed = seed;
+                     return css_scan_locked(ctx, ch, 1, av, bv, ap, bp, wsize, wstep, treshold, runs, 0, mds,
+                                            window_set, o0, o1, s, nullptr, X);
                    });
 }
 

@@ -56,6 +56,11 @@ extern "C" int gd_pack_shape(const int *apos, const int *bpos, int alen, int ble
   *asize = alen > 0 ? popsize(apos, alen) : 0;
   *bsize = blen > 0 ? popsize(bpos, blen) : 0;
   *nrows = (*asize > 0 && *bsize > 0) ? (alen / *asize < blen / *bsize ? alen / *asize : blen / *bsize) : 0;
+  /* a partial trailing row, or A and B holding different row counts, has no packed form
+   * (the reference layout reads B past A's rows: GD_ERR_BOUNDS in its scans) */
+  if ((int64_t)*nrows * *asize != alen || (int64_t)*nrows * *bsize != blen)
+    return pk_fail(GD_ERR_ARG, "the tracks do not consist of whole rows of asize / bsize individuals "
+                               "(both populations, the same row count)");
   return GD_OK;
 }
 

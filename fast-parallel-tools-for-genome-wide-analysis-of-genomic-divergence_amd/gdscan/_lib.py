@@ -32,7 +32,7 @@ GD_FET_EXACT = 1
 EXPORTS = (
     "gd_fet_threadcompute", "gd_fet_compute", "gd_fet_scan_host", "gd_fet_scan_host_ex",
     "gd_set_fet_mode", "gd_get_fet_mode", "gd_fet_scan_device_ex", "gd_fet_scan_host_batch_ex",
-    "gd_css_threadcompute", "gd_css_compute", "gd_css_scan_host", "gd_css_scan_host_ex",
+    "gd_css_threadcompute", "gd_css_compute", "gd_css_scan_host", "gd_css_scan_host_ex", "gd_css_coords_host",
     "gd_ctx_create", "gd_ctx_destroy", "gd_window_count",
     "gd_fet_scan_device", "gd_css_scan_device", "gd_css_scan_device_ex", "gd_fet_scan_host_batch",
     "gd_css_scan_host_batch", "gd_css_scan_host_batch_ex",
@@ -94,6 +94,9 @@ def _load() -> C.CDLL:
     lib.gd_css_scan_host.argtypes = [dp, dp, ip, ip, i32, i32, i32, i32, i32, i32, i32, C.c_uint64, i32, dp, dp]
     lib.gd_css_scan_host_ex.argtypes = [dp, dp, ip, ip, i32, i32, i32, i32, i32, i32, i32, i32, i32, C.c_uint64, i32,
                                         dp, dp]
+    lib.gd_css_coords_host.argtypes = [dp, dp, ip, ip, i32, i32, i32, i32, i32, i32, i32, i32, C.c_uint64, i32, dp,
+                                       dp, dp]
+    lib.gd_css_coords_host.restype = C.c_int
     lib.gd_ctx_create.argtypes = [i32]
     lib.gd_ctx_create.restype = vp
     lib.gd_ctx_destroy.argtypes = [vp]

@@ -57,3 +57,24 @@ def scan(avals, bvals, apos, bpos, regend, wsize=2500, wstep=500, treshold=10, r
                                   GD_WINDOWS_SERIAL if serial else GD_WINDOWS_THREADED,
                                   scores.ctypes.data_as(_DP), p.ctypes.data_as(_DP)))
     return scores, p
+
+
+def scan_coords(avals, bvals, apos, bpos, regend, wsize=2500, wstep=500, treshold=10, runs=100, seed=None,
+                serial=False, mds=0):
+    """Diagnostics (gd_css_coords_host): ``scan`` plus the coordinates the permutation test
+    read, shape (regend // wstep, asize + bsize, 2); rows of uncomputed windows are zero."""
+    nwin = int(regend) // int(wstep)
+    scores = np.zeros(nwin)
+    p = np.zeros(nwin)
+    (av, bv, ap, bp), scores, p = _ptrs(avals, bvals, apos, bpos, scores, p, "p")
+    # get_population_size (comparative.c:25-34): the leading run of pos[0]
+    m = int(np.argmax(ap != ap[0]) or ap.shape[0]) + int(np.argmax(bp != bp[0]) or bp.shape[0])
+    X = np.zeros((max(nwin, 1), m, 2))
+    s = lib.gd_get_seed() if seed is None else int(seed)
+    check(lib.gd_css_coords_host(av.ctypes.data_as(_DP), bv.ctypes.data_as(_DP), ap.ctypes.data_as(_IP),
+                                 bp.ctypes.data_as(_IP), int(regend), int(wsize), int(wstep), av.shape[0],
+                                 bv.shape[0], int(treshold), int(runs), int(mds), s,
+                                 GD_WINDOWS_SERIAL if serial else GD_WINDOWS_THREADED,
+                                 scores.ctypes.data_as(_DP), p.ctypes.data_as(_DP), X.ctypes.data_as(_DP)))
+    X[:nwin][scores == 0] = 0.0
+    return scores, p, X[:nwin]

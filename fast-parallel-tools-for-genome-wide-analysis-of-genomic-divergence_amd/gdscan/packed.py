@@ -60,8 +60,12 @@ def shape(apos, bpos):
     bp = np.ascontiguousarray(bpos, dtype=np.int32)
     a, b, n = C.c_int(), C.c_int(), C.c_int()
     ip = C.POINTER(C.c_int)
-    check(lib.gd_pack_shape(ap.ctypes.data_as(ip), bp.ctypes.data_as(ip), ap.shape[0], bp.shape[0], C.byref(a),
-                            C.byref(b), C.byref(n)))
+    st = lib.gd_pack_shape(ap.ctypes.data_as(ip), bp.ctypes.data_as(ip), ap.shape[0], bp.shape[0], C.byref(a),
+                           C.byref(b), C.byref(n))
+    if st == GD_ERR_ARG and n.value >= 0 and a.value > 0 and b.value > 0:
+        raise ValueError("the tracks do not consist of whole rows of asize / bsize individuals "
+                         f"({a.value} + {b.value} individuals, {ap.shape[0]} + {bp.shape[0]} elements)")
+    check(st)
     return a.value, b.value, n.value
 
 

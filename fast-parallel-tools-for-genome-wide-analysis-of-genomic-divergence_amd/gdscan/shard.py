@@ -54,3 +54,33 @@ def gather_tracks(local, shards, windows_per_chrom, group=None):
             track[offs[c]:offs[c] + n] = out[r * pad + pos: r * pad + pos + n]
             pos += n
     return track
+
+
+def default_store():
+    """The key-value store of the default process group (c10d TCPStore under torchrun)."""
+    import torch.distributed as dist
+    return dist.distributed_c10d._get_default_store()
+
+
+def queue_pull(store, key, n_items, work):
+    """Dynamic chromosome queue across ranks: the reference's mutex-guarded task counter
+    (threadcss.c:226-232, threadfisher.c:191-201) lifted to one process per GPU.  Each rank
+    takes the next ticket from the store's atomic counter `key` and runs work(ticket) until
+    all n_items are taken, so ranks whose chromosomes cost more (C5's early-exit
+    permutations) simply pull fewer.  Returns the tickets this rank ran, in order."""
+    done = []
+    while True:
+        k = int(store.add(key, 1)) - 1
+        if k >= n_items:
+            return done
+        work(k)
+        done.append(k)
+
+
+def gather_lists(items, group=None):
+    """All-gather one variable-length list of ints per rank (tiny; CPU tensors over the
+    default group's backend are not needed: uses all_gather_object)."""
+    import torch.distributed as dist
+    out = [None] * dist.get_world_size(group)
+    dist.all_gather_object(out, [int(x) for x in items], group=group)
+    return out

@@ -92,6 +92,16 @@ int gd_css_scan_host_ex(const double *avals, const double *bvals, const int *apo
                         int wsize, int wstep, int alen, int blen, int treshold, int runs, int drosophila, int mds,
                         uint64_t seed, int window_set, double *scores, double *p);
 
+/* diagnostics: gd_css_scan_host_ex (count metric, runs > 0 and treshold > 0, else GD_ERR_ARG)
+ * that also returns the coordinates its permutation test read (the classical-MDS X of
+ * css.c:545-556, or SMACOF's for mds 1 / 2): X (host) holds gd_window_count(...) rows of
+ * 2 (asize + bsize) doubles, point i of window w at X[w * 2m + 2i], X[w * 2m + 2i + 1]; rows
+ * of windows with scores[w] == 0 are unspecified.  Lets a test re-run significance_treshold
+ * (css.c:727-752) on the device's own X, isolating the permutation kernel from the solver. */
+int gd_css_coords_host(const double *avals, const double *bvals, const int *apos, const int *bpos, int regend,
+                       int wsize, int wstep, int alen, int blen, int treshold, int runs, int mds, uint64_t seed,
+                       int window_set, double *scores, double *p, double *X);
+
 /* ---- device-resident batched scans (all pointers are device pointers except `chroms`) ---- */
 typedef struct gd_chrom {
   int64_t a_off, b_off; /* element offsets of this chromosome in avals/apos and bvals/bpos */
@@ -161,7 +171,9 @@ typedef struct gd_pchrom {
   uint64_t seed;
 } gd_pchrom;
 /* get_population_size() of both tracks (comparative.c:25-34) and the number of rows both
- * hold whole (min(alen / asize, blen / bsize)); host memory */
+ * hold whole (min(alen / asize, blen / bsize)); host memory.  GD_ERR_ARG (outputs still
+ * set) unless alen = nrows * asize and blen = nrows * bsize: a partial row or unequal row
+ * counts have no packed form */
 int gd_pack_shape(const int *apos, const int *bpos, int alen, int blen, int *asize, int *bsize, int *nrows);
 /* packs nrows rows (host memory; outputs hold nrows * GD_PACK_WORDS(size) words and nrows
  * positions).  GD_ERR_ARG when a value is not one of the four codes or an individual's

@@ -247,6 +247,76 @@ double orc_css_significance(const double *S, int m, int *tracks, int asize, int 
   return (hits + 1) * 1.0 / (nscores + 1);
 }
 
+/* significance_treshold (css.c:727-752) of one window on given coordinates X (m x 2):
+ * S = calc_dist(X), the observed score css() of the identity tracks, then the literal
+ * shuffle / css() / hits loop with identity start tracks and the window's nrand48 state.
+ * For the isolated permutation test (tests/test_css_perm_isolated.py), which feeds it the
+ * device's own X: a permuted score within tie_rel * (|observed| + the observed score's
+ * term magnitudes) of the observed one is a near tie, whose hit decision depends on the
+ * summation order.  p_lo / p_hi resolve every near tie as a miss / as a hit (p is
+ * monotone in the set of hits, so any consistent resolution lies in [p_lo, p_hi]);
+ * *p is the literal `new >= score` decision; *nties counts the near ties seen before both
+ * resolutions stopped. */
+void orc_css_perm_from_x(const double *X, int asize, int bsize, int treshold, int runs, uint64_t state48,
+                         double tie_rel, double *score, double *p, double *p_lo, double *p_hi, int *nties) {
+  int m = asize + bsize, i, n;
+  double *S = malloc(sizeof(double) * m * m);
+  int *tracks = malloc(sizeof(int) * m), *atr = malloc(sizeof(int) * asize), *btr = malloc(sizeof(int) * bsize);
+  int h_ex = 0, n_ex = 0, h_lo = 0, n_lo = 0, h_hi = 0, n_hi = 0, d_ex, d_lo, d_hi, ties = 0;
+  unsigned short st[3];
+  double sc, tol, bet = 0, ad = 0, bd = 0;
+  orc_css_dist(X, m, S);
+  for (i = 0; i < asize; i++) atr[i] = i;
+  for (i = 0; i < bsize; i++) btr[i] = asize + i;
+  sc = orc_css_score(S, m, atr, btr, asize, bsize);
+  /* the magnitudes of the observed score's terms (every S entry is >= 0) */
+  for (i = 0; i < asize; i++)
+    for (n = 0; n < bsize; n++) bet += S[i * m + asize + n];
+  for (i = 0; i + 1 < asize; i++) ad += S[i * m + i + 1];
+  for (i = 0; i + 1 < bsize; i++) bd += S[(asize + i) * m + asize + i + 1];
+  tol = tie_rel * (fabs(sc) + bet / (asize * bsize) +
+                   (asize + bsize) * (asize > 1 ? ad / (asize * asize * (asize - 1.0)) : 0.0) +
+                   (asize + bsize) * (bsize > 1 ? bd / (bsize * bsize * (bsize - 1.0)) : 0.0));
+  for (i = 0; i < m; i++) tracks[i] = i;
+  orc_state_words(state48, st);
+  d_ex = d_lo = d_hi = !(treshold > 0 && runs > 0);
+  for (n = 0; n < runs && !(d_ex && d_lo && d_hi); n++) {
+    double v, diff;
+    for (i = m - 1; i > 0; i--) {
+      int r = (int)orc_randint_css(i + 1, st), t = tracks[i];
+      tracks[i] = tracks[r];
+      tracks[r] = t;
+    }
+    v = orc_css_score(S, m, tracks, tracks + asize, asize, bsize);
+    diff = v - sc;
+    if (fabs(diff) <= tol && !(d_lo && d_hi)) ties++;
+    if (!d_ex) {
+      h_ex += v >= sc;
+      n_ex++;
+      d_ex = h_ex >= treshold || n_ex >= runs;
+    }
+    if (!d_lo) {
+      h_lo += diff > tol;
+      n_lo++;
+      d_lo = h_lo >= treshold || n_lo >= runs;
+    }
+    if (!d_hi) {
+      h_hi += diff >= -tol;
+      n_hi++;
+      d_hi = h_hi >= treshold || n_hi >= runs;
+    }
+  }
+  *score = sc;
+  *p = (h_ex + 1) * 1.0 / (n_ex + 1);
+  *p_lo = (h_lo + 1) * 1.0 / (n_lo + 1);
+  *p_hi = (h_hi + 1) * 1.0 / (n_hi + 1);
+  *nties = ties;
+  free(S);
+  free(tracks);
+  free(atr);
+  free(btr);
+}
+
 /* one window: returns 1 and fills score/p, or 0 when fill_averages discards it */
 int orc_css_window(const double *av, const double *bv, int asize, int bsize, int npos, int treshold, int runs,
                    uint64_t state48, double *score, double *p, int *nperm) {

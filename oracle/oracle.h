@@ -34,6 +34,8 @@ void orc_css_dist(const double *X, int m, double *S);
 double orc_css_score(const double *S, int m, const int *atr, const int *btr, int asize, int bsize);
 double orc_css_significance(const double *S, int m, int *tracks, int asize, int bsize, double score, int treshold,
                             int runs, unsigned short st[3], int *nperm);
+void orc_css_perm_from_x(const double *X, int asize, int bsize, int treshold, int runs, uint64_t state48,
+                         double tie_rel, double *score, double *p, double *p_lo, double *p_hi, int *nties);
 int orc_css_window(const double *av, const double *bv, int asize, int bsize, int npos, int treshold, int runs,
                    uint64_t state48, double *score, double *p, int *nperm);
 int orc_css_scan(const double *avals, const double *bvals, const int *apos, const int *bpos, int regend, int wsize,

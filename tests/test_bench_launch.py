@@ -1,0 +1,29 @@
+"""CPU: bench.py's launcher and distributed plumbing without a GPU.  `bench.py --gpus 2`
+with no torch.distributed environment starts torch.distributed.run itself (before any GPU
+call); --backend gloo --dry-run then runs the shard plan, the shared chromosome queue over
+the default store (the C5 leg's load balancing) and the (score, p) track gather."""
+import json
+import os
+import subprocess
+import sys
+
+from conftest import ROOT
+
+
+def test_bench_spawns_ranks_and_gathers():
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["MASTER_ADDR"] = "127.0.0.1"
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--backend", "gloo", "--dry-run",
+                        "--c45-chroms", "4"], capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = lines[0]
+    assert out["dry_run"] and out["n_gpus"] == 2 and out["gather_ok"]
+    assert sum(out["queue_per_rank"]) == 8 and out["static_per_rank"] == [4, 4]
+
+
+def test_bench_single_rank_needs_no_launcher():
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--dry-run"], capture_output=True, text=True,
+                       timeout=120, cwd=ROOT)
+    assert r.returncode == 0 and json.loads(r.stdout.strip().splitlines()[-1])["n_gpus"] == 1

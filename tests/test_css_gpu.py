@@ -29,6 +29,10 @@ def _cmp_scores(s, s_ref, rel=1e-9):
 
 @pytest.mark.parametrize("asize,bsize,nsnp", [(10, 10, 60_000), (20, 20, 30_000), (7, 13, 30_000), (40, 40, 4_000),
                                               (1, 1, 20_000), (33, 31, 6_000), (45, 45, 3_000),
+                                              # the two-windows-per-wave p40 tier below m = 40: partial rows
+                                              # of window B in lanes 40-63 and in the LDS tail quads
+                                              (12, 13, 8_000), (15, 16, 8_000), (16, 17, 8_000), (19, 20, 8_000),
+                                              (13, 14, 8_000), (5, 30, 8_000),
                                               # the one-wave 80 tier: 1, 8 and 9 tail rows (m = 65, 72, 73)
                                               (33, 32, 3_000), (30, 42, 3_000), (43, 30, 3_000)])
 def test_scores_match_oracle(oracle, asize, bsize, nsnp):
@@ -66,16 +70,19 @@ def test_permutation_p_matches_oracle(oracle, asize, bsize, treshold, runs, nsnp
     assert np.all(p[~comp] == 0)
 
 
-@pytest.mark.parametrize("asize,bsize,nsnp", [(8, 8, 20_000), (40, 40, 3_000)])
-def test_irregular_values_take_the_literal_path(oracle, asize, bsize, nsnp):
+@pytest.mark.parametrize("asize,bsize,nsnp,nbad", [(8, 8, 20_000, 400), (40, 40, 3_000, 400), (20, 20, 10_000, 40),
+                                                   (13, 14, 10_000, 40), (33, 40, 3_000, 30)])
+def test_irregular_values_take_the_literal_path(oracle, asize, bsize, nsnp, nbad):
     """Values outside {3,0,-3,-10000} (including NaN and huge values) follow the
-    reference predicate (int)v_i * v_j == -9 with x86 cast semantics."""
+    reference predicate (int)v_i * v_j == -9 with x86 cast semantics.  With few bad
+    values most windows stay on the popcount build, so literal and popcount windows
+    share the two-window waves of the p40 tier."""
     from gdscan import css
     av, bv, ap, bp, regend = _synth(6, nsnp, asize, bsize)
     rng = np.random.default_rng(0)
     for arr in (av, bv):
-        idx = rng.choice(len(arr), 400, replace=False)
-        arr[idx] = rng.choice([1.0, -1.0, 9.0, -9.0, 4.5, -2.25, 0.5, -18.0, np.nan, 1e10, -3.0000001], 400)
+        idx = rng.choice(len(arr), nbad, replace=False)
+        arr[idx] = rng.choice([1.0, -1.0, 9.0, -9.0, 4.5, -2.25, 0.5, -18.0, np.nan, 1e10, -3.0000001], nbad)
     s, p = css.scan(av, bv, ap, bp, regend)
     s_ref, p_ref = oracle_css_scan(oracle, av, bv, ap, bp, regend)
     _cmp_scores(s, s_ref)
@@ -141,6 +148,50 @@ def test_device_batch_api_matches_host(oracle):
         n = regend // 500
         _cmp_scores(sc[w:w + n], s_ref)
         assert (pv[w:w + n] == p_ref).mean() >= 0.99
+        w += n
+
+
+@pytest.mark.parametrize("shapes", [
+    # p40 tier: different (a, b) splits and m inside one two-window wave at every
+    # chromosome boundary; odd per-chromosome window counts shift the pairing, and the
+    # batch's total is odd (the last wave holds one window)
+    [(20, 20, 5_001), (12, 13, 3_007), (19, 20, 2_203), (15, 16, 4_111), (25, 8, 2_600)],
+    # tiers 24 and 64/80 mixed with smaller cohorts in one batch
+    [(10, 10, 3_001), (4, 7, 2_500), (40, 40, 1_300), (30, 20, 1_500)],
+])
+def test_device_batch_mixed_cohorts(oracle, shapes):
+    import torch
+    from gdscan import _lib, synth
+    from gdscan._lib import Chrom, check, lib
+    dev = torch.device("cuda", 0)
+    data = [synth.chromosome(50 + c, n, a, b) for c, (a, b, n) in enumerate(shapes)]
+    A = np.concatenate([x[0] for x in data]); B = np.concatenate([x[1] for x in data])
+    AP = np.concatenate([x[2] for x in data]); BP = np.concatenate([x[3] for x in data])
+    chroms = (Chrom * len(data))()
+    off_a = off_b = w = 0
+    total = 0
+    for i, (av, bv, ap, bp, regend) in enumerate(data):
+        chroms[i].a_off, chroms[i].b_off, chroms[i].alen, chroms[i].blen = off_a, off_b, len(av), len(bv)
+        chroms[i].regend, chroms[i].w_out, chroms[i].seed = regend, w, 3000 + i
+        off_a += len(av); off_b += len(bv); w += regend // 500
+        total += lib.gd_window_count(regend, 2500, 500, _lib.GD_WINDOWS_THREADED)
+    if shapes[0] == (20, 20, 5_001):
+        assert total % 2 == 1
+    tens = [torch.from_numpy(x).to(dev) for x in (A, B, AP, BP)]
+    sc = torch.zeros(w, dtype=torch.float64, device=dev); pv = torch.zeros_like(sc)
+    ctx = lib.gd_ctx_create(0)
+    check(lib.gd_css_scan_device(ctx, chroms, len(data), *[t.data_ptr() for t in tens], 2500, 500, 10, 60,
+                                 _lib.GD_WINDOWS_THREADED, sc.data_ptr(), pv.data_ptr(),
+                                 torch.cuda.current_stream().cuda_stream))
+    lib.gd_ctx_destroy(ctx)
+    sc = sc.cpu().numpy(); pv = pv.cpu().numpy()
+    w = 0
+    for i, (av, bv, ap, bp, regend) in enumerate(data):
+        s_ref, p_ref = oracle_css_scan(oracle, av, bv, ap, bp, regend, runs=60, seed=3000 + i)
+        n = regend // 500
+        _cmp_scores(sc[w:w + n], s_ref)
+        comp = s_ref != 0
+        assert (pv[w:w + n][comp] == p_ref[comp]).mean() >= 0.99, i
         w += n
 
 

@@ -266,3 +266,20 @@ def test_mid_size_windows_counting_rank(oracle):
     s_ref, d_ref = oracle_fet_scan(oracle, av, bv, ap, bp, regend, seed=5)
     assert (s_ref != 0).sum() > 500
     assert close(s, s_ref) and close(d, d_ref)
+
+
+@pytest.mark.parametrize("name", ["10x10", "20x20", "7x13_w1000", "small_serial", "perc50"])
+def test_golden_reference_fixtures(name):
+    """The HIP scan against the committed outputs of the reference's own C
+    (tests/golden/make_golden.py: threadcompute / compute scores, the seeded
+    fisher_exact_test stddev), with no oracle in between."""
+    from conftest import SCAN_FIXTURES, load_scan_fixture
+    from gdscan import fet
+    assert name in SCAN_FIXTURES
+    f = load_scan_fixture(name)
+    s, d = fet.scan(f["av"], f["bv"], f["ap"], f["bp"], f["regend"], f["wsize"], f["wstep"], f["perc"],
+                    seed=f["seed"], serial=f["serial"])
+    assert (f["scores"] != 0).sum() > 50
+    assert np.array_equal(s == 0, f["scores"] == 0)
+    assert close(s, f["scores"]) and close(d, f["stddev"])
+    assert np.mean(s == f["scores"]) > 0.99

@@ -66,7 +66,10 @@ def test_shape_is_get_population_size():
     ap = np.repeat(np.array([5, 9, 12], dtype=np.int32), 4)
     bp = np.repeat(np.array([5, 9, 12], dtype=np.int32), 3)
     assert packed.shape(ap, bp) == (4, 3, 3)
-    assert packed.shape(ap[:-1], bp) == (4, 3, 2)
+    with pytest.raises(ValueError, match="whole rows"):  # partial trailing row: no packed form
+        packed.shape(ap[:-1], bp)
+    with pytest.raises(ValueError, match="whole rows"):  # A and B hold different row counts
+        packed.shape(ap, bp[:-3])
 
 
 @pytest.mark.gpu
@@ -108,6 +111,24 @@ def test_packed_css_equals_reference_layout(mds, runs):
         s_ref, p_ref = css.scan(av, bv, ap, bp, regend, treshold=10, runs=runs, mds=mds, seed=5)
         assert (s_ref != 0).sum() > 200
         assert np.array_equal(s, s_ref) and np.array_equal(p, p_ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("a,b", [(45, 33), (33, 45), (64, 40)])
+def test_packed_multiword_rows(a, b):
+    """Rows wider than one 64-bit word (more than 32 individuals per population): the
+    per-word popcounts of k_snp_fet_packed and the word select of k_css_pack_codes."""
+    from gdscan import css, fet, packed
+    av, bv, ap, bp, regend = _synth(60, 3_000, a, b)
+    pc = packed.pack(av, bv, ap, bp, regend)
+    assert pc.acodes.shape[0] == 3_000 * ((a + 31) // 32)
+    (s, d), = packed.fet_scan([pc], seed=11)
+    s_ref, d_ref = fet.scan(av, bv, ap, bp, regend, seed=11)
+    assert (s_ref != 0).sum() > 50  # >= 68 individuals: the reference's overflow NaNs included
+    assert np.array_equal(s, s_ref, equal_nan=True) and np.array_equal(d, d_ref, equal_nan=True)
+    (s, p), = packed.css_scan([pc], treshold=10, runs=40, seed=11)
+    s_ref, p_ref = css.scan(av, bv, ap, bp, regend, treshold=10, runs=40, seed=11)
+    assert np.array_equal(s, s_ref, equal_nan=True) and np.array_equal(p, p_ref)
 
 
 @pytest.mark.gpu
