@@ -40,3 +40,6 @@ torch.cuda.synchronize()
 dt = (time.perf_counter() - t) / steps
 print(f"CSS {nch}x{nsnp} {a}+{b} runs={runs}: {nwin} windows, {dt*1e3:.2f} ms/step, {nwin/dt/1e6:.2f} M windows/s, stages {_lib.last_stage_ms()}")
 s = sc.cpu().numpy(); print("computed", (s != 0).sum(), "nan", np.isnan(s).sum(), "mean p", pv.cpu().numpy()[s != 0].mean())
+import json
+print(json.dumps({"css_time": True, "nch": nch, "nsnp": nsnp, "pop": a, "runs": runs, "treshold": tres,
+                  "windows_per_scan": int(nwin), "scans": steps + 1, "ms_per_step": dt * 1e3}))

@@ -1,70 +1,114 @@
-"""Turn a tools/profile_round.sh output directory into the committed profiles/ files:
-  profiles/<R>_kernel_stats.csv   rocprofv3 --stats summary of the bench command
+"""Turn a tools/profile_r03.sh output directory into the committed profiles/ files:
+  profiles/<R>_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary of the bench command
   profiles/<R>_bench.json         the bench line measured in the same call
-  profiles/<R>_fet_traffic.json   HBM bytes per FET scan from the PMC passes
-  profiles/<R>_fet_valu.json      VALU wave-instructions per FET scan (SQ_INSTS_VALU)
-  profiles/<R>_summary.md         per-kernel averages, per-scan traffic, cross-checks
+  profiles/<R>_ubench_valu.json   VALU issue rates per instruction (tools/ubench_valu.hip), the peak
+  profiles/<R>_fet_traffic.json   HBM bytes per FET scan from the FETCH_SIZE / WRITE_SIZE passes
+  profiles/<R>_fet_valu.json      VALU wave-instructions per FET scan (SQ_INSTS_VALU) + SQ cycles
+  profiles/<R>_css_valu.json      VALU wave-instructions per window of the kernels each CSS leg
+                                  dispatches: c3 (k_css_pack + k_css_mds_p40), c4 (k_css_pack +
+                                  k_css_mds_t80), c5_perm (k_css_perm<80>)
+  profiles/<R>_summary.md         per-kernel averages, per-scan traffic and instruction counts
+Every kernel a figure is built from must be present in its counter file: a missing one
+(e.g. a renamed kernel) stops the script instead of silently dropping out of a sum.
 """
 import csv
 import json
 import shutil
+import statistics
 import sys
 from collections import defaultdict
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parent.parent
-R = sys.argv[1] if len(sys.argv) > 1 else "r02"
+R = sys.argv[1] if len(sys.argv) > 1 else "r03"
 src = ROOT / "gpurun_out" / R
 dst = ROOT / "profiles"
 dst.mkdir(exist_ok=True)
 
 FET_KERNELS = ("k_popsize", "k_bounds", "k_snp_fet", "k_fet_")
+SQ = ("SQ_INSTS_VALU", "SQ_ACTIVE_INST_VALU", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_WAVES", "SQ_INSTS_LDS",
+      "SQ_LDS_BANK_CONFLICT", "SQ_ACTIVE_INST_LDS")
 
 
 def short(name):
-    return name.split("(")[0].replace("void ", "")
+    return name.split("(")[0].replace("void ", "").strip()
 
 
 def find(d, suffix):
     hits = sorted(Path(d).rglob(f"*{suffix}"))
-    return hits[0] if hits else None
+    if not hits:
+        raise SystemExit(f"no *{suffix} under {d}")
+    return hits[0]
 
 
-def counters(d, counter):
+def counters(d):
+    """{kernel: {counter: sum over dispatches}}, {kernel: dispatches}"""
     f = find(d, "counter_collection.csv")
-    per = defaultdict(float)
-    n = defaultdict(int)
+    per = defaultdict(lambda: defaultdict(float))
+    disp = defaultdict(set)
     for row in csv.DictReader(open(f)):
-        if row["Counter_Name"] != counter:
-            continue
         k = short(row["Kernel_Name"])
-        per[k] += float(row["Counter_Value"])
-        n[k] += 1
-    return per, n
+        per[k][row["Counter_Name"]] += float(row["Counter_Value"])
+        disp[k].add(row["Dispatch_Id"])
+    return per, {k: len(v) for k, v in disp.items()}
+
+
+def need(per, names, where):
+    missing = [n for n in names if n not in per]
+    if missing:
+        raise SystemExit(f"{where}: kernels {missing} absent from the counters (have {sorted(per)})")
+
+
+def last_json(path):
+    for line in reversed(Path(path).read_text().strip().splitlines()):
+        if line.startswith("{"):
+            return json.loads(line)
+    raise SystemExit(f"no JSON line in {path}")
 
 
 stats = find(src / "ktrace", "kernel_stats.csv")
 shutil.copy(stats, dst / f"{R}_kernel_stats.csv")
-bench = json.loads((src / "bench.json").read_text().strip().splitlines()[-1])
+bench = last_json(src / "bench.json")
 (dst / f"{R}_bench.json").write_text(json.dumps(bench, indent=1) + "\n")
 
-fetch, nf = counters(src / "pmc_fetch", "FETCH_SIZE")
-write, nw = counters(src / "pmc_write", "WRITE_SIZE")
-scans = nf.get("k_popsize", 0)
-fk = {k: v for k, v in fetch.items() if k.startswith(FET_KERNELS)}
-wk = {k: v for k, v in write.items() if k.startswith(FET_KERNELS)}
-# rocprofv3 reports FETCH_SIZE / WRITE_SIZE in KiB; gfx950 FETCH_SIZE counts half of
-# a wide coalesced read (MI355X_MICROARCH.md, HBM section): double it
+# ---- VALU issue peak (tools/ubench_valu.hip: 8 waves per SIMD, 8 independent chains per lane)
+rates = {}
+for line in (src / "ubench_valu.txt").read_text().splitlines():
+    parts = line.split()
+    if len(parts) >= 2:
+        try:
+            rates[" ".join(parts[:-1]) if parts[-1] != "Tlane-op/s" else parts[0]] = float(
+                parts[-2] if parts[-1] == "Tlane-op/s" else parts[-1])
+        except ValueError:
+            pass
+ginst = {k: v * 1e12 / 64 / 1e9 for k, v in rates.items()}
+simple = [ginst[k] for k in ("v_add_u32", "v_sub_u32", "v_and_b32", "v_lshrrev_b32", "v_max_i32", "v_mul_f32")
+          if k in ginst]
+if not simple:
+    raise SystemExit("ubench_valu.txt holds no simple-op rates")
+peak = statistics.median(simple)
+ub = {"peak_ginsts": peak, "method": "tools/ubench_valu.hip on the box: median issue rate of v_add_u32, v_sub_u32, "
+      "v_and_b32, v_lshrrev_b32, v_max_i32, v_mul_f32 (8 waves per SIMD, 8 independent chains per lane)",
+      "ginsts_per_op": ginst, "tlane_ops_per_op": rates,
+      "cycles_per_wave_inst_per_simd": {k: 256 * 4 * 2.4 / v for k, v in ginst.items() if v > 0}}
+(dst / f"{R}_ubench_valu.json").write_text(json.dumps(ub, indent=1) + "\n")
+
+# ---- FET HBM traffic and VALU per scan
+fetch, nf = counters(src / "pmc_fetch")
+write, _ = counters(src / "pmc_write")
+need(fetch, ["k_popsize", "k_bounds", "k_fet_window_fast"], "pmc_fetch")
+scans = nf["k_popsize"]
+fk = {k: v["FETCH_SIZE"] for k, v in fetch.items() if k.startswith(FET_KERNELS)}
+wk = {k: v["WRITE_SIZE"] for k, v in write.items() if k.startswith(FET_KERNELS)}
+# rocprofv3 reports FETCH_SIZE / WRITE_SIZE in KiB; gfx950 FETCH_SIZE counts half of a wide
+# coalesced read (MI355X_MICROARCH.md, HBM section): double it
 fetch_b = 2 * 1024 * sum(fk.values()) / scans
 write_b = 1024 * sum(wk.values()) / scans
 cfg = bench["config"]
+config = [cfg["chromosomes_per_gpu"], cfg["snps_per_gpu"] // cfg["chromosomes_per_gpu"], cfg["asize"], cfg["bsize"]]
 traffic = {
-    "config": [cfg["chromosomes_per_gpu"], cfg["snps_per_gpu"] // cfg["chromosomes_per_gpu"], cfg["asize"],
-               cfg["bsize"]],
-    "bytes_per_scan": fetch_b + write_b,
-    "fetch_bytes_per_scan": fetch_b,
-    "write_bytes_per_scan": write_b,
-    "scans": scans,
+    "config": config, "bytes_per_scan": fetch_b + write_b, "fetch_bytes_per_scan": fetch_b,
+    "write_bytes_per_scan": write_b, "scans": scans,
     "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes over the FET scan kernels; "
               "KiB -> bytes, FETCH_SIZE x2 (gfx950 wide-read correction)",
     "per_kernel_kib_per_scan": {k: {"fetch": fk.get(k, 0) / scans, "write": wk.get(k, 0) / scans}
@@ -72,61 +116,67 @@ traffic = {
 }
 (dst / f"{R}_fet_traffic.json").write_text(json.dumps(traffic, indent=1) + "\n")
 
-valu, nv = counters(src / "pmc_valu", "SQ_INSTS_VALU")
-vscans = nv.get("k_popsize", 0)
+valu, nv = counters(src / "pmc_valu")
+need(valu, ["k_popsize", "k_bounds", "k_fet_window_fast"], "pmc_valu")
+vscans = nv["k_popsize"]
 vk = {k: v for k, v in valu.items() if k.startswith(FET_KERNELS)}
 valu_doc = {
-    "config": traffic["config"],
-    "valu_wave_insts_per_scan": sum(vk.values()) / vscans,
+    "config": config,
+    "valu_wave_insts_per_scan": sum(v["SQ_INSTS_VALU"] for v in vk.values()) / vscans,
     "scans": vscans,
-    "method": "rocprofv3 --pmc SQ_INSTS_VALU over the FET scan kernels (wave-instructions)",
-    "per_kernel_per_scan": {k: v / vscans for k, v in sorted(vk.items())},
+    "method": "rocprofv3 --pmc SQ_INSTS_VALU (+ SQ cycle counters) over the FET scan kernels (wave-instructions)",
+    "per_kernel_per_scan": {k: {c: v.get(c, 0.0) / vscans for c in SQ} for k, v in sorted(vk.items())},
 }
 (dst / f"{R}_fet_valu.json").write_text(json.dumps(valu_doc, indent=1) + "\n")
 
-# CSS (C3 shape): VALU wave-instructions per call of the bit-plane pass and the m = 40 MDS kernel
-cval, ncv = counters(src / "pmc_css_valu", "SQ_INSTS_VALU")
-mds = [k for k in cval if k.startswith("k_css_mds<40")]
-css_doc = None
-if mds and ncv.get("k_css_pack", 0):
-    per_call = cval[mds[0]] / ncv[mds[0]] + cval["k_css_pack"] / ncv["k_css_pack"]
-    css_doc = {"config": traffic["config"], "valu_wave_insts_per_scan": per_call,
-               "method": "rocprofv3 --pmc SQ_INSTS_VALU over k_css_pack + k_css_mds<40, 1> (wave-instructions "
-                         "per call = per C3 scan)"}
-    (dst / f"{R}_css_valu.json").write_text(json.dumps(css_doc, indent=1) + "\n")
+# ---- CSS legs: wave-instructions per window of the kernels each leg dispatches
+css_doc = {}
 
-# CSS permutations (C5 shape, tools/css_time.py): SQ counters of k_css_perm per dispatch
-perm_doc = None
-if (src / "pmc_perm").exists():
-    pc = defaultdict(float)
-    pd = set()
-    for row in csv.DictReader(open(find(src / "pmc_perm", "counter_collection.csv"))):
-        if short(row["Kernel_Name"]).startswith("k_css_perm"):
-            pc[row["Counter_Name"]] += float(row["Counter_Value"])
-            pd.add(row["Dispatch_Id"])
-    if pd:
-        per = {k: v / len(pd) for k, v in pc.items()}
-        perm_doc = {"config": "1 chromosome x 500000 SNPs, 40+40, mcT=10, mcR=1000 (tools/css_time.py)",
-                    "per_dispatch": per,
-                    "method": "rocprofv3 --pmc SQ_* over k_css_perm<80> (one dispatch per scan)"}
-        (dst / f"{R}_perm_pmc.json").write_text(json.dumps(perm_doc, indent=1) + "\n")
 
+def css_entry(key, d, kernels, windows, what):
+    per, nd = counters(d)
+    need(per, kernels, d.name)
+    ipw = sum(per[k]["SQ_INSTS_VALU"] / nd[k] for k in kernels) / windows
+    css_doc[key] = {"kernels": kernels, "windows_per_dispatch": windows, "valu_wave_insts_per_window": ipw,
+                    "method": f"rocprofv3 --pmc SQ_INSTS_VALU ... over {' + '.join(kernels)} ({what}); "
+                              "wave-instructions per dispatch / windows per dispatch",
+                    "per_kernel_per_dispatch": {k: {c: per[k].get(c, 0.0) / nd[k] for c in SQ} for k in kernels}}
+
+
+c3b = last_json(src / "pmc_c3.json")
+css_entry("c3", src / "pmc_c3", ["k_css_pack", "k_css_mds_p40"], c3b["css"]["config"]["windows_per_gpu"],
+          "bench.py C3 leg: 20 x 500k SNPs, 20+20, runs=0")
+c4t = last_json(src / "pmc_c4.txt")
+css_entry("c4", src / "pmc_c4", ["k_css_pack", "k_css_mds_t80"], c4t["windows_per_scan"],
+          "tools/css_time.py: 4 x 500k SNPs, 40+40, runs=0")
+c5t = last_json(src / "pmc_c5.txt")
+css_entry("c5_perm", src / "pmc_c5", ["k_css_perm<80>"], c5t["windows_per_scan"],
+          "tools/css_time.py: 1 x 500k SNPs, 40+40, mcT=10, mcR=1000")
+(dst / f"{R}_css_valu.json").write_text(json.dumps(css_doc, indent=1) + "\n")
+
+# ---- summary
 rows = list(csv.DictReader(open(stats)))
-lines = [f"# {R} profile summary", "", "Command: `rocprofv3 --kernel-trace --stats -- python3 bench.py --steps 5 "
-         "--warmup 1 --no-cpu` (FET + CSS legs), PMC passes separate (tools/profile_round.sh).", "",
+lines = [f"# {R} profile summary", "",
+         "Commands: tools/profile_r03.sh (bench line; `rocprofv3 --kernel-trace --stats -- python3 bench.py --steps 5 "
+         "--warmup 1 --no-cpu --c45-steps 1`; PMC passes in runs of their own).", "",
          "| kernel | calls | avg us | total ms |", "|---|---|---|---|"]
 for r in rows:
     lines.append(f"| {short(r['Name'])} | {r['Calls']} | {float(r['AverageNs']) / 1e3:.1f} | "
                  f"{float(r['TotalDurationNs']) / 1e6:.2f} |")
 alg = bench["roofline"]["alg_bytes_per_step"]
-lines += ["", f"FET scan HBM traffic (PMC): {traffic['bytes_per_scan'] / 1e9:.3f} GB per scan "
+scan_ms = bench["roofline"]["stage_ms"]["scan_total"]
+lines += ["", f"VALU issue peak (ubench, median of simple ops): {peak:.0f} G wave-instructions/s "
+          f"= {256 * 4 * 2.4 / peak:.2f} cycles per wave64 instruction per SIMD at 2.4 GHz. Per op: "
+          + ", ".join(f"{k} {v:.0f}" for k, v in ginst.items()) + ".",
+          "", f"FET scan HBM traffic (PMC): {traffic['bytes_per_scan'] / 1e9:.3f} GB per scan "
           f"(fetch {fetch_b / 1e9:.3f} + write {write_b / 1e9:.3f}); algorithmic B = {alg / 1e9:.3f} GB.",
           "", f"FET scan VALU (PMC SQ_INSTS_VALU): {valu_doc['valu_wave_insts_per_scan'] / 1e9:.3f} G wave-instructions "
-          f"per scan; at the bench's scan time that is {valu_doc['valu_wave_insts_per_scan'] / (bench['roofline']['stage_ms']['scan_total'] * 1e-3) / 1e9:.0f} "
-          "G/s of the 614 G/s issue peak (256 CUs x 4 SIMDs x 2.4 GHz / 4).",
-          "", "Bench line (same call):", "", "```", json.dumps(bench), "```"]
-if perm_doc:
-    lines[-5:-5] = ["", "k_css_perm<80> per dispatch (PMC): " + ", ".join(
-        f"{k} {v:.4g}" for k, v in sorted(perm_doc["per_dispatch"].items()))]
+          f"per scan = {valu_doc['valu_wave_insts_per_scan'] / (scan_ms * 1e-3) / 1e9:.0f} G/s at the bench's scan time "
+          f"({scan_ms:.3f} ms), {valu_doc['valu_wave_insts_per_scan'] / (scan_ms * 1e-3) / 1e9 / peak:.2f} of the "
+          "measured issue peak.", ""]
+for k, v in css_doc.items():
+    lines.append(f"CSS {k}: {v['valu_wave_insts_per_window']:.0f} VALU wave-instructions per window "
+                 f"({' + '.join(v['kernels'])}).")
+lines += ["", "Bench line (same call):", "", "```", json.dumps(bench), "```"]
 (dst / f"{R}_summary.md").write_text("\n".join(lines) + "\n")
-print("\n".join(lines[:40]))
+print("\n".join(lines[:60]))
