@@ -386,3 +386,70 @@ int orc_css_scan(const double *avals, const double *bvals, const int *apos, cons
   }
   return 0;
 }
+
+/* The reference's own permutation convention (Q9), for the statistical check of
+ * deviation 1: css.c compute() (css.c:49-156) keeps ONE nrand48 state for the whole scan
+ * (seeded from time(NULL) at css.c:111-114; here from state48) and ONE `signtracks`
+ * array that every window's significance_treshold keeps shuffling (css.c:739), so each
+ * window's permutations start from the previous window's last shuffle.  Window set and
+ * scores as orc_css_scan (serial = compute(), else threadcompute()'s windows visited in
+ * order, as one thread would). */
+int orc_css_scan_chained(const double *avals, const double *bvals, const int *apos, const int *bpos, int regend,
+                         int wsize, int wstep, int alen, int blen, int treshold, int runs, uint64_t state48,
+                         int serial, double *scores, double *p) {
+  int asize = orc_population_size(apos, alen), bsize = orc_population_size(bpos, blen);
+  int wend = serial ? orc_serial_window_end(regend, wsize, wstep) : orc_threaded_window_end(regend, wsize, wstep);
+  int w, i, m = asize + bsize, la[2] = {0, 0}, lb[2] = {0, 0};
+  int *signtracks, *atr, *btr;
+  double *D, *S, *X;
+  unsigned short st[3];
+  if (alen <= 0 || blen <= 0) return 0;
+  signtracks = malloc(sizeof(int) * m);
+  atr = malloc(sizeof(int) * asize);
+  btr = malloc(sizeof(int) * bsize);
+  D = malloc(sizeof(double) * m * m);
+  S = malloc(sizeof(double) * m * m);
+  X = malloc(sizeof(double) * m * 2);
+  for (i = 0; i < m; i++) signtracks[i] = i;
+  for (i = 0; i < asize; i++) atr[i] = i;
+  for (i = 0; i < bsize; i++) btr[i] = asize + i;
+  orc_state_words(state48, st);
+  for (w = 0; w < wend; w++) {
+    int start = w * wstep, stop = start + wsize, npos, l, r;
+    l = la[0];
+    r = la[1];
+    while (l < alen && apos[l] < start) l++;
+    while (r < alen && apos[r] <= stop) r++;
+    la[0] = l;
+    la[1] = r;
+    l = lb[0];
+    r = lb[1];
+    while (l < blen && bpos[l] < start) l++;
+    while (r < blen && bpos[r] <= stop) r++;
+    lb[0] = l;
+    lb[1] = r;
+    npos = (la[1] - la[0]) / asize;
+    if (npos <= 0) continue;
+    if ((long)lb[0] + (long)npos * bsize > blen) {
+      w = -1;
+      break;
+    }
+    orc_css_compare_all(avals + la[0], bvals + lb[0], asize, bsize, npos, D);
+    if (!orc_css_fill_averages(D, m)) continue;
+    orc_css_cmds(D, m, X, NULL);
+    orc_css_dist(X, m, S);
+    {
+      double sc = orc_css_score(S, m, atr, btr, asize, bsize);
+      if (sc == -1) continue;
+      scores[w] = sc;
+      p[w] = orc_css_significance(S, m, signtracks, asize, bsize, sc, treshold, runs, st, NULL);
+    }
+  }
+  free(signtracks);
+  free(atr);
+  free(btr);
+  free(D);
+  free(S);
+  free(X);
+  return w < 0 ? ORC_ERR_BOUNDS : 0;
+}

@@ -42,6 +42,10 @@ int orc_css_scan(const double *avals, const double *bvals, const int *apos, cons
                  int wstep, int alen, int blen, int treshold, int runs, uint64_t seed, int serial, double *scores,
                  double *p);
 
+int orc_css_scan_chained(const double *avals, const double *bvals, const int *apos, const int *bpos, int regend,
+                         int wsize, int wstep, int alen, int blen, int treshold, int runs, uint64_t state48,
+                         int serial, double *scores, double *p);
+
 /* CSS options (css_options_oracle.c) */
 void orc_css_compare_freq(const double *av, const double *bv, int npos, double *D);
 double orc_css_stress(const double *delta, const double *D, int m);
