@@ -67,8 +67,8 @@ int gd_css_launch(int mp, int drosophila, int mds, const gd_chrom_dev *d_ch, int
                   uint32_t *planes, const int32_t *lo_a, const int32_t *hi_a, const int32_t *lo_b,
                   const double *avals, const double *bvals, const int64_t *word_off, const uint64_t *acodes,
                   const uint64_t *bcodes, int64_t wtotal, int64_t max_rows_words, int treshold, int runs,
-                  double *scores, double *p, double *xbuf, uint8_t *status, unsigned *flags, hipStream_t s,
-                  hipEvent_t ev_perm);
+                  double *scores, double *p, double *xbuf, uint8_t *status, unsigned *flags, double *slab,
+                  hipStream_t s, hipEvent_t ev_perm);
 int gd_synth_launch(int chrom, int nsnp, int asize, int bsize, uint64_t seed, const double *freq_table,
                     double *avals, double *bvals, int32_t *apos, int32_t *bpos, hipStream_t s);
 
@@ -822,7 +822,9 @@ static int css_scan_locked(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, cons
     max_words = std::max(max_words, std::max(wa * d.asize, wb * d.bsize));
   }
   const int mp = gd_css_tier(mmax);
-  if (mp == 0) return fail(GD_ERR_SIZE, "asize + bsize above the largest supported CSS tier (128)");
+  if (mp == 0) return fail(GD_ERR_SIZE, "asize + bsize above the largest supported cohort (GD_CSS_BIG_MAX = 512)");
+  /* the general path (m above the register tiers): one matrix slab per workgroup */
+  const int64_t slab_doubles = mp > GD_CSS_TIER_MAX ? gd_css_big_grid(pl.wtotal) * gd_css_big_slab_per_wg(mp) : 1;
   if (drosophila)
     for (int c = 0; c < nchrom; ++c) {
       const gd_chrom_dev &d = pl.h[c];
@@ -831,19 +833,21 @@ static int css_scan_locked(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, cons
                                 "(asize = bsize = 1; compare_freq, css.c:245-264)");
     }
   const bool perms = (runs > 0 && treshold > 0) || mds == 2; /* xbuf/status carry coordinates */
-  auto layout2 = [&](Carve &k, gd_css_planes **d_pl, uint32_t **planes, double **xbuf, uint8_t **status) {
+  auto layout2 = [&](Carve &k, gd_css_planes **d_pl, uint32_t **planes, double **xbuf, uint8_t **status,
+                     double **slab) {
     layout1(k, &d_ch, &flags, &lo_a, &hi_a, &lo_b);
     *d_pl = k.take<gd_css_planes>(nchrom);
     *planes = k.take<uint32_t>(std::max<int64_t>(words, 1));
     *xbuf = k.take<double>(perms ? pl.wtotal * 2 * mp : 1);
     *status = k.take<uint8_t>(perms ? pl.wtotal : 1);
+    *slab = k.take<double>(slab_doubles);
   };
   gd_css_planes *d_pl;
   uint32_t *planes;
-  double *xbuf;
+  double *xbuf, *slab;
   uint8_t *status;
   Carve cv2{nullptr};
-  layout2(cv2, &d_pl, &planes, &xbuf, &status);
+  layout2(cv2, &d_pl, &planes, &xbuf, &status, &slab);
   if (cv2.off > ctx->ws_cap) {
     /* growing reallocates: keep the pass-1 results (descriptors, flags, bounds) */
     char *old = ctx->ws;
@@ -859,7 +863,7 @@ static int css_scan_locked(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, cons
   }
   {
     Carve real{ctx->ws};
-    layout2(real, &d_pl, &planes, &xbuf, &status);
+    layout2(real, &d_pl, &planes, &xbuf, &status, &slab);
   }
   HIP_TRY(hipMemcpyAsync(d_ch, pl.h.data(), sizeof(gd_chrom_dev) * nchrom, hipMemcpyHostToDevice, s));
   HIP_TRY(hipMemcpyAsync(d_pl, hp.data(), sizeof(gd_css_planes) * nchrom, hipMemcpyHostToDevice, s));
@@ -868,7 +872,7 @@ static int css_scan_locked(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, cons
   HIP_TRY(hipEventRecord(ctx->ev[1], s));
   st = gd_css_launch(mp, drosophila, mds, d_ch, nchrom, d_pl, planes, lo_a, hi_a, lo_b, avals, bvals, d_woff,
                      pk ? pk->acodes : nullptr, pk ? pk->bcodes : nullptr, pl.wtotal, max_words, treshold, runs,
-                     scores, p, xbuf, status, flags, s, ctx->ev[2]);
+                     scores, p, xbuf, status, flags, slab, s, ctx->ev[2]);
   if (st) return fail(st, "CSS kernel launch failed");
   HIP_TRY(hipEventRecord(ctx->ev[3], s));
   if (x_out && perms) {

@@ -2619,17 +2619,345 @@ __global__ void __launch_bounds__(64, CSS_P40_WAVES)
   CSS_PROF(6);
 }
 
+/* ------------------------------------------------------------------------ */
+/* The general path: cohorts above the register tiers (GD_CSS_TIER_MAX < m <=  */
+/* GD_CSS_BIG_MAX; the reference scores any m, threadcss.c:191,207-215).  The    */
+/* same algorithm as k_css_mds -- compare_all by popcounts (literal predicate for */
+/* irregular windows), fill_averages, double centering, Householder (dsytd2,      */
+/* lower), bisection for the top two eigenvalues, inverse iteration, back-        */
+/* transformation, X, css -- with thread i owning row i and the matrix in a       */
+/* global-memory slab of the workgroup's own, column-major (element (i, j) at     */
+/* j ld + i): every sweep over a column touches one contiguous 8 m-byte run, so a */
+/* wave's loads coalesce, and the slab (m ld doubles) stays cache-resident.  The  */
+/* workgroups loop over windows (grid = number of slabs).                         */
+/* ------------------------------------------------------------------------ */
+template <int MP>
+__global__ void __launch_bounds__(MP)
+    k_css_mds_big(const gd_chrom_dev *ch, int nchrom, const gd_css_planes *pl, const uint32_t *planes,
+                  const int32_t *lo_a_, const int32_t *hi_a_, const int32_t *lo_b_, const double *avals,
+                  const double *bvals, int64_t wtotal, int want_x, int force_literal, int xstride, double *scores,
+                  double *pvals, double *xbuf, uint8_t *status, unsigned *flags, double *slab, int64_t slab_per_wg,
+                  int ld) {
+  constexpr int NT = MP, NW = MP / 64;
+  __shared__ double s_row[MP + 2];
+  __shared__ double s_v[MP], s_w[MP];
+  __shared__ __attribute__((aligned(16))) double s_d[MP + 4];
+  __shared__ __attribute__((aligned(16))) double s_e2[MP + 4];
+  __shared__ double s_e[MP], s_tau[MP];
+  __shared__ uint64_t s_mask[2 * MP];
+  __shared__ double s_y[2][MP];
+  __shared__ double s_lu[2][3][MP];
+  __shared__ uint8_t s_piv[2][MP];
+  __shared__ double s_x[2 * MP];
+  __shared__ int s_tr[MP];
+  __shared__ double s_lam[2];
+  __shared__ double s_red[2 * (2 * NW + 2)];
+
+  const int tid = threadIdx.x, i = tid;
+  double *A = slab + (int64_t)blockIdx.x * slab_per_wg;
+  auto at = [&](int r, int c) -> double & { return A[(int64_t)c * ld + r]; };
+  s_tr[tid] = tid;
+
+  for (int64_t w = blockIdx.x; w < wtotal; w += gridDim.x) {
+    const int c = chrom_of(ch, nchrom, w);
+    const gd_chrom_dev &d = ch[c];
+    const int a = d.asize, b = d.bsize, m = a + b;
+    const int64_t wl = w - d.w_base;
+    const int32_t la = lo_a_[w], ha = hi_a_[w], lb = lo_b_[w];
+    const int npos = (ha - la) / a;
+    if (npos <= 0) continue;
+    if ((int64_t)lb + (int64_t)npos * b > d.blen) {
+      if (tid == 0) atomicOr(flags, GD_FLAG_B_BOUNDS);
+      continue;
+    }
+    if (m > MP || m > ld) {
+      if (tid == 0) atomicOr(flags, GD_FLAG_BAD_SIZE);
+      continue;
+    }
+    const bool row = i < m;
+    const gd_css_planes P = pl[c];
+    const uint32_t *pa = planes + P.pa, *pb = planes + P.pb;
+    const int64_t ra = la / a, rb = lb / b;
+    __syncthreads(); /* the previous window's readers of s_x / s_tr are done */
+
+    /* ---- regular window?  (rows aligned and no value outside {3,0,-3,-10000}) */
+    bool literal = force_literal || (la % a) != 0 || (lb % b) != 0;
+    if (!literal) {
+      int irr = 0;
+      for (int k = tid; k * 64 < npos; k += NT) {
+        const int nb = min(64, npos - 64 * k);
+        const uint64_t tail = nb == 64 ? ~0ull : ((1ull << nb) - 1);
+        const uint64_t xa = plane_bits64(pa + (int64_t)(2 * a) * P.wa, ra + 64 * k) & tail;
+        const uint64_t xb = plane_bits64(pb + (int64_t)(2 * b) * P.wb, rb + 64 * k) & tail;
+        irr |= (xa | xb) != 0;
+      }
+      literal = __syncthreads_or(irr);
+    }
+
+    /* ---- compare_all into column-major A (counts as doubles; the diagonal is 0) */
+    if (!literal) {
+      for (int k = 0; k * 64 < npos; ++k) {
+        const int nb = min(64, npos - 64 * k);
+        const uint64_t tail = nb == 64 ? ~0ull : ((1ull << nb) - 1);
+        __syncthreads();
+        if (row) {
+          const uint32_t *base = i < a ? pa + (int64_t)(2 * i) * P.wa : pb + (int64_t)(2 * (i - a)) * P.wb;
+          const int64_t nw = i < a ? P.wa : P.wb;
+          const int64_t r = (i < a ? ra : rb) + 64 * k;
+          s_mask[2 * i] = plane_bits64(base, r) & tail;
+          s_mask[2 * i + 1] = plane_bits64(base + nw, r) & tail;
+        }
+        __syncthreads();
+        if (row) {
+          const uint64_t Pi = s_mask[2 * i], Ni = s_mask[2 * i + 1];
+          for (int j = 0; j < m; ++j) {
+            const double cnt = (double)(__popcll(Pi & s_mask[2 * j + 1]) + __popcll(Ni & s_mask[2 * j]));
+            at(i, j) = k == 0 ? cnt : at(i, j) + cnt;
+          }
+        }
+      }
+    } else if (row) {
+      const double *av = avals + d.a_off + la, *bv = bvals + d.b_off + lb;
+      auto val = [&](int r, int k) { return r < a ? av[(int64_t)k * a + r] : bv[(int64_t)k * b + (r - a)]; };
+      for (int j = 0; j < m; ++j) {
+        int cnt = 0;
+        /* the reference casts the row element of the larger index within a population and
+         * the A element across populations (css.c:281-326); the diagonal never counts */
+        const bool cast_i = ((i < a) == (j < a)) ? (i > j) : (i < a);
+        if (j != i)
+          for (int k = 0; k < npos; ++k) {
+            const double vi = val(i, k), vj = val(j, k);
+            const double prod = cast_i ? x86_int(vi) * vj : x86_int(vj) * vi;
+            cnt += prod == -9.0;
+          }
+        at(i, j) = (double)cnt;
+      }
+    }
+
+    /* ---- fill_averages: entries < 1e-5 (diagonal included) count as unknown */
+    double zero_tol;
+    {
+      double unv = 0.0, sum = 0.0;
+      if (row)
+        for (int j = 0; j < m; ++j) {
+          const double x = at(i, j);
+          if (x < 0.00001)
+            unv += 1.0;
+          else
+            sum += x;
+        }
+      block_sum2<NW>(unv, sum, s_red); /* sums of integers: exact in any order */
+      const int tot = m * m;
+      if ((int)unv > tot / 2) continue; /* discarded window: outputs untouched */
+      const double avg = sum / tot;
+      /* B = -1/2 Z (D o D) Z by double centering, as k_css_mds */
+      double rs = 0.0;
+      if (row)
+        for (int j = 0; j < m; ++j) {
+          double x = at(i, j);
+          x = fma(avg, 1.0 - fmin(x, 1.0), x);
+          x = x * x;
+          at(i, j) = x;
+          rs += x;
+        }
+      const double ri = row ? rs / m : 0.0;
+      s_v[i] = ri;
+      const double g = block_sum<NW>(ri, s_red) / m;
+      __syncthreads();
+      double f2 = 0.0;
+      if (row)
+        for (int j = 0; j < m; ++j) {
+          const double x = -0.5 * ((at(i, j) - (ri + s_v[j])) + g);
+          at(i, j) = x;
+          f2 = fma(x, x, f2);
+        }
+      zero_tol = 64.0 * m * DBL_EPSILON * sqrt(block_sum<NW>(f2, s_red));
+    }
+
+    /* ---- Householder tridiagonalisation (dsytd2, lower), the k_css_mds step on the slab;
+     * after step k column k holds the reflector v_k */
+    for (int k = 0; k < m; ++k) {
+      __syncthreads();
+      /* row k right of the diagonal (zeros at j <= k) and d_k; A(k, j) as lane k holds it */
+      if (row) s_row[i] = i > k ? at(k, i) : 0.0;
+      if (i == k) s_d[k] = at(k, k);
+      __syncthreads();
+      if (k >= m - 2) {
+        if (tid == 0 && k == m - 2) s_e[k] = s_row[k + 1];
+        continue;
+      }
+      const double xi = (i > k + 1 && row) ? s_row[i] : 0.0;
+      const double alpha = s_row[k + 1];
+      double praw = 0.0, ak1 = 0.0;
+      if (i > k && row) {
+        double p0 = 0.0, p1 = 0.0;
+        int j = k + 1;
+        for (; j + 1 < m; j += 2) {
+          p0 = fma(at(i, j), s_row[j], p0);
+          p1 = fma(at(i, j + 1), s_row[j + 1], p1);
+        }
+        if (j < m) p0 = fma(at(i, j), s_row[j], p0);
+        praw = p0 + p1;
+        ak1 = at(i, k + 1);
+      }
+      double sigma = xi * xi, q = (i > k && row) ? s_row[i] * praw : 0.0;
+      if (i == k + 1) {
+        s_red[2 * NW] = praw;
+        s_red[2 * NW + 1] = ak1;
+      }
+      block_sum2<NW>(sigma, q, s_red);
+      const double pr1 = s_red[2 * NW], a11 = s_red[2 * NW + 1];
+      double tau = 0.0, beta = alpha, scale = 0.0;
+      if (sigma != 0.0) {
+        beta = -copysign(sqrt(alpha * alpha + sigma), alpha);
+        const double r = fast_rcp(beta * (alpha - beta));
+        tau = -(alpha - beta) * (alpha - beta) * r;
+        scale = beta * r;
+      }
+      /* v = scale (x - beta e_{k+1}), v_{k+1} = 1;  p = tau A v;  w = p + K v */
+      const double vi = (i == k + 1) ? 1.0 : xi * scale;
+      const double pi = (i > k && row) ? (tau * scale) * fma(-beta, ak1, praw) : 0.0;
+      const double K = -0.5 * tau * (tau * scale * scale) * fma(beta, fma(beta, a11, -2.0 * pr1), q);
+      const double wi = fma(K, vi, pi);
+      if (tid == 0) {
+        s_e[k] = beta;
+        s_tau[k] = tau;
+      }
+      s_v[i] = vi;
+      s_w[i] = wi;
+      __syncthreads();
+      if (i > k && row)
+        for (int j = k + 1; j < m; ++j) at(i, j) = fma(-vi, s_w[j], fma(-wi, s_v[j], at(i, j)));
+      if (row) at(i, k) = vi; /* stash v_k in the dead column k */
+    }
+    __syncthreads();
+
+    /* ---- the two largest eigenvalues of T (as k_css_mds) */
+    double glo, ghi;
+    {
+      double lo = DBL_MAX, hi = -DBL_MAX;
+      if (row) {
+        const double r = (i > 0 ? fabs(s_e[i - 1]) : 0.0) + (i < m - 1 ? fabs(s_e[i]) : 0.0);
+        lo = s_d[i] - r;
+        hi = s_d[i] + r;
+      }
+      for (int t = tid; t < MP + 4; t += NT) s_e2[t] = (t >= 1 && t < m) ? s_e[t - 1] * s_e[t - 1] : 0.0;
+      glo = block_reduce<NW, OpMin>(lo, s_red);
+      ghi = block_reduce<NW, OpMax>(hi, s_red);
+      const double pad = 2.0 * DBL_EPSILON * fmax(fabs(glo), fabs(ghi)) * m + DBL_MIN;
+      glo -= pad;
+      ghi += pad;
+      for (int t = tid; t < MP + 4; t += NT)
+        if (t >= m) s_d[t] = 2.0 * fabs(ghi) + 2.0 * fabs(glo) + 1.0;
+    }
+    const double bis_tol = CSS_BISECT_TOL * fmax(fabs(glo), fabs(ghi)) + DBL_MIN;
+    __syncthreads();
+    if (tid < 64) bisect_top2(m, glo, ghi, bis_tol, s_d, s_e2, s_lam, tid);
+    __syncthreads();
+
+    /* ---- eigenvectors of T: two inverse-iteration solves, orthogonalised */
+    if (tid < 2) invit_factor<MP>(m, tid, s_d, s_e, s_lam, s_lu, s_x, s_piv, s_y);
+    __syncthreads();
+    if (row) {
+      const double tiny = DBL_EPSILON * fmax(fmax(fabs(glo), fabs(ghi)), DBL_MIN);
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const double u0 = s_lu[e][0][i];
+        s_lu[e][0][i] = fast_rcp(u0 == 0.0 ? tiny : u0);
+      }
+    }
+    double y1 = 0.0, y2 = 0.0;
+    for (int itn = 0; itn < 2; ++itn) {
+      __syncthreads();
+      if (tid < 2) invit_solve<MP>(m, tid, s_lu, s_x, s_piv, s_y);
+      __syncthreads();
+      y1 = row ? s_y[0][i] : 0.0;
+      y2 = row ? s_y[1][i] : 0.0;
+      double n1 = y1 * y1, n2 = y2 * y2;
+      block_sum2<NW>(n1, n2, s_red);
+      y1 *= 1.0 / sqrt(n1);
+      y2 *= 1.0 / sqrt(n2);
+      __syncthreads();
+      if (itn == 0 && row) {
+        s_y[0][i] = y1;
+        s_y[1][i] = y2;
+      }
+    }
+    {
+      double dt = y1 * y2, zero = 0.0;
+      block_sum2<NW>(dt, zero, s_red);
+      y2 = fma(-dt, y1, y2);
+      double n2 = y2 * y2;
+      zero = 0.0;
+      block_sum2<NW>(n2, zero, s_red);
+      y2 *= 1.0 / sqrt(n2);
+    }
+    {
+      __syncthreads();
+      if (row) {
+        s_y[0][i] = y1;
+        s_y[1][i] = y2;
+      }
+      __syncthreads();
+      double t1 = 0.0, t2 = 0.0;
+      if (row) {
+        const double el = i > 0 ? s_e[i - 1] : 0.0, er = i + 1 < m ? s_e[i] : 0.0;
+        const int il = i > 0 ? i - 1 : 0, ir = i + 1 < m ? i + 1 : i;
+        t1 = y1 * (s_d[i] * y1 + el * s_y[0][il] + er * s_y[0][ir]);
+        t2 = y2 * (s_d[i] * y2 + el * s_y[1][il] + er * s_y[1][ir]);
+      }
+      block_sum2<NW>(t1, t2, s_red);
+      if (tid == 0) {
+        s_lam[0] = fabs(t1) <= zero_tol ? 0.0 : t1;
+        s_lam[1] = fabs(t2) <= zero_tol ? 0.0 : t2;
+      }
+      __syncthreads();
+    }
+
+    /* ---- back-transformation y <- H_0 H_1 ... H_{m-3} y (v_k in column k) */
+    for (int k = m - 3; k >= 0; --k) {
+      const double vk = row ? at(i, k) : 0.0;
+      const double t = s_tau[k];
+      double d1 = vk * y1, d2 = vk * y2;
+      block_sum2<NW>(d1, d2, s_red);
+      y1 = fma(-(t * d1), vk, y1);
+      y2 = fma(-(t * d2), vk, y2);
+    }
+
+    /* ---- X = Q sqrt(L) (css.c:545-556), then calc_dist + css on identity groups */
+    {
+      const double L1 = sqrt(s_lam[0]), L2 = sqrt(s_lam[1]);
+      __syncthreads();
+      if (row) {
+        s_x[2 * i] = y1 * L1 + y2 * 0.0;
+        s_x[2 * i + 1] = y1 * 0.0 + y2 * L2;
+      }
+      __syncthreads();
+    }
+    const double score = css_score<NW>(s_tr, a, b, [&](int p, int q) { return xdist(s_x, p, q); }, s_red);
+    if (score == -1.0) continue; /* the reference's "discarded" marker (css.c:127) */
+    if (tid == 0) {
+      scores[d.w_out + wl] = score;
+      if (!want_x) pvals[d.w_out + wl] = 1.0; /* runs == 0: p = (0 + 1) / (0 + 1) */
+    }
+    if (want_x) {
+      for (int e = tid; e < xstride; e += NT) xbuf[w * xstride + e] = (e < 2 * m) ? s_x[e] : 0.0;
+      if (tid == 0) status[w] = 1;
+    }
+  }
+}
+
 /* the other stages of a scan (gd_css_perm.hip, gd_css_smacof.hip, gd_packed.hip) */
 int gd_packed_css_planes_launch(const gd_chrom_dev *d_ch, int nchrom, const gd_css_planes *d_pl,
                                 const int64_t *word_off, const uint64_t *acodes, const uint64_t *bcodes,
                                 int64_t max_rows_words, uint32_t *planes, hipStream_t s);
 int gd_css_perm_launch(int mp, const gd_chrom_dev *d_ch, int nchrom, const double *xbuf, const uint8_t *status,
-                       int64_t wtotal, int treshold, int runs, double *p, unsigned *wq, hipStream_t s);
+                       int64_t wtotal, int treshold, int runs, double *p, unsigned *wq, double *slab, hipStream_t s);
 int gd_css_smacof_launch(int mp, bool freq, const gd_chrom_dev *d_ch, int nchrom, const gd_css_planes *d_pl,
                          const uint32_t *planes, const int32_t *lo_a, const int32_t *hi_a, const int32_t *lo_b,
                          const double *avals, const double *bvals, int64_t wtotal, int mds, int want_x,
                          int force_literal, double *scores, double *p, double *xbuf, uint8_t *status,
-                         unsigned *flags, hipStream_t s);
+                         unsigned *flags, double *slab, hipStream_t s);
 int gd_css_freq_cmds_launch(int mp, const gd_chrom_dev *d_ch, int nchrom, const int32_t *lo_a, const int32_t *hi_a,
                             const int32_t *lo_b, const double *avals, const double *bvals, int64_t wtotal,
                             int want_x, double *scores, double *p, double *xbuf, uint8_t *status, unsigned *flags,
@@ -2640,7 +2968,26 @@ int gd_css_tier(int m) {
   static const int tiers[] = {24, 40, 64, 80, 96, 128};
   for (int t : tiers)
     if (m <= t) return t;
+  /* the general path: any tier value above GD_CSS_TIER_MAX, the xbuf row width / 2 */
+  if (m <= GD_CSS_BIG_MAX) return (m + 7) & ~7;
   return 0;
+}
+
+static int launch_big(int mp, const gd_chrom_dev *d_ch, int nchrom, const gd_css_planes *d_pl, const uint32_t *planes,
+                      const int32_t *lo_a, const int32_t *hi_a, const int32_t *lo_b, const double *avals,
+                      const double *bvals, int64_t wtotal, int want_x, int force_literal, double *scores, double *p,
+                      double *xbuf, uint8_t *status, unsigned *flags, double *slab, hipStream_t s) {
+  const int ld = gd_css_big_ld(mp);
+  const int64_t per = gd_css_big_slab_per_wg(mp), grid = gd_css_big_grid(wtotal);
+  if (mp <= 256)
+    hipLaunchKernelGGL(k_css_mds_big<256>, dim3((unsigned)grid), dim3(256), 0, s, d_ch, nchrom, d_pl, planes, lo_a,
+                       hi_a, lo_b, avals, bvals, wtotal, want_x, force_literal, 2 * mp, scores, p, xbuf, status, flags,
+                       slab, per, ld);
+  else
+    hipLaunchKernelGGL(k_css_mds_big<512>, dim3((unsigned)grid), dim3(512), 0, s, d_ch, nchrom, d_pl, planes, lo_a,
+                       hi_a, lo_b, avals, bvals, wtotal, want_x, force_literal, 2 * mp, scores, p, xbuf, status, flags,
+                       slab, per, ld);
+  return hipGetLastError() == hipSuccess ? GD_OK : GD_ERR_HIP;
 }
 
 static int launch_p40(const gd_chrom_dev *d_ch, int nchrom, const gd_css_planes *d_pl, const uint32_t *planes,
@@ -2684,8 +3031,8 @@ int gd_css_launch(int mp, int drosophila, int mds, const gd_chrom_dev *d_ch, int
                   uint32_t *planes, const int32_t *lo_a, const int32_t *hi_a, const int32_t *lo_b,
                   const double *avals, const double *bvals, const int64_t *word_off, const uint64_t *acodes,
                   const uint64_t *bcodes, int64_t wtotal, int64_t max_rows_words, int treshold, int runs,
-                  double *scores, double *p, double *xbuf, uint8_t *status, unsigned *flags, hipStream_t s,
-                  hipEvent_t ev_perm) {
+                  double *scores, double *p, double *xbuf, uint8_t *status, unsigned *flags, double *slab,
+                  hipStream_t s, hipEvent_t ev_perm) {
   const bool perms = runs > 0 && treshold > 0;
   const int want_x1 = (perms || mds == 2) ? 1 : 0; /* coordinates out of the classical stage */
   const char *fl = getenv("GD_CSS_FORCE_LITERAL"); /* diagnostics: per-SNP predicate for every window */
@@ -2748,7 +3095,9 @@ int gd_css_launch(int mp, int drosophila, int mds, const gd_chrom_dev *d_ch, int
         CSS_TIER(96, 2)
         CSS_TIER(128, 2)
         default:
-          return GD_ERR_SIZE;
+          if (mp <= GD_CSS_TIER_MAX || mp > GD_CSS_BIG_MAX) return GD_ERR_SIZE;
+          st = launch_big(mp, d_ch, nchrom, d_pl, planes, lo_a, hi_a, lo_b, avals, bvals, wtotal, want_x1, force_literal,
+                          scores, p, xbuf, status, flags, slab, s);
       }
 #undef CSS_TIER
     }
@@ -2756,10 +3105,10 @@ int gd_css_launch(int mp, int drosophila, int mds, const gd_chrom_dev *d_ch, int
   }
   if (mds != 0) {
     st = gd_css_smacof_launch(mp, drosophila != 0, d_ch, nchrom, d_pl, planes, lo_a, hi_a, lo_b, avals, bvals, wtotal,
-                              mds, perms ? 1 : 0, force_literal, scores, p, xbuf, status, flags, s);
+                              mds, perms ? 1 : 0, force_literal, scores, p, xbuf, status, flags, slab, s);
     if (st) return st;
   }
   if (ev_perm && hipEventRecord(ev_perm, s) != hipSuccess) return GD_ERR_HIP; /* end of the MDS stage */
-  if (perms) st = gd_css_perm_launch(mp, d_ch, nchrom, xbuf, status, wtotal, treshold, runs, p, flags + 8, s);
+  if (perms) st = gd_css_perm_launch(mp, d_ch, nchrom, xbuf, status, wtotal, treshold, runs, p, flags + 8, slab, s);
   return st;
 }

@@ -700,6 +700,215 @@ __global__ void __launch_bounds__(PermShape<MP>::NT) PERM_WPE
   }
 }
 
+/* ------------------------------------------------------------------------ */
+/* The general path (GD_CSS_TIER_MAX < m <= GD_CSS_BIG_MAX): one workgroup of 4 */
+/* waves per window (pulled from the work counter), 64 permutations per pass.    */
+/* Wave 0 draws them (lane q: Fisher-Yates on its own 16-bit LDS column, start   */
+/* state by jump-ahead, the serial stream when a draw is rejected, as            */
+/* k_css_perm); the workgroup composes F_q = F_{q-1} o sigma_q row-parallel (one */
+/* barrier per step, F_q written over sigma_q); each wave scores every fourth     */
+/* track in FP64 with the lanes splitting the a b between-group pairs (S in the   */
+/* workgroup's global slab, computed once per window from X); hits are counted in */
+/* permutation order, so the early exit stops where the serial loop stops.  The   */
+/* observed score is the same function of the identity tracks.                    */
+/* ------------------------------------------------------------------------ */
+namespace {
+constexpr int PB_P = 64; /* permutations per pass */
+
+/* Fisher-Yates of random_shuffle (css.c:700-706) on column `col` (stride PB_P), draws
+ * from state x without rejection; true if a draw would have been rejected */
+__device__ __forceinline__ bool fy_big_fast(uint16_t *col, uint64_t x, int m, const uint32_t *mag) {
+  bool rej = false;
+  uint64_t y = x << 16;
+  for (int s = 0; s < m - 1; ++s) {
+    const int n = __builtin_amdgcn_readfirstlane(m - s);
+    const gd_randint rd = perm_rd((uint32_t)n, __builtin_amdgcn_readfirstlane(mag[n]));
+    y = y * GD_LCG_A + (GD_LCG_C << 16);
+    const uint32_t r = (uint32_t)(y >> 33);
+    rej |= r > rd.limit;
+    const int j = (int)(r - (__umulhi(r, rd.magic) >> rd.shift) * (uint32_t)n);
+    const uint16_t u = col[(n - 1) * PB_P], v = col[j * PB_P];
+    col[(n - 1) * PB_P] = v;
+    col[j * PB_P] = u;
+  }
+  return rej;
+}
+
+/* the same with random_int_nrand48's redraw loop (css.c:675-690) */
+__device__ __forceinline__ void fy_big_exact(uint16_t *col, uint64_t x, int m, const uint32_t *mag) {
+  for (int s = 0; s < m - 1; ++s) {
+    const int n = __builtin_amdgcn_readfirstlane(m - s);
+    const gd_randint rd = perm_rd((uint32_t)n, __builtin_amdgcn_readfirstlane(mag[n]));
+    uint32_t r;
+    do {
+      x = gd_lcg_next(x);
+      r = gd_lcg_value(x);
+    } while (r > rd.limit);
+    const int j = (int)gd_randint_mod(&rd, r);
+    const uint16_t u = col[(n - 1) * PB_P], v = col[j * PB_P];
+    col[(n - 1) * PB_P] = v;
+    col[j * PB_P] = u;
+  }
+}
+
+__device__ __forceinline__ double pb_wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+/* css() (css.c:608-647) of one track array by one wave: S(x, y) at y ld + x */
+template <class TRK>
+__device__ __forceinline__ double pb_score(TRK track, const double *S, int ld, int a, int b, double inva, double invb,
+                                           int lane) {
+  const int ab = a * b, m = a + b;
+  double bet = 0.0, wa = 0.0, wb = 0.0;
+  int ii = lane / b, jj = lane - (lane / b) * b;
+#pragma unroll 4
+  for (int p = lane; p < ab; p += 64) {
+    bet += S[(int64_t)track(a + jj) * ld + track(ii)];
+    jj += 64;
+    while (jj >= b) {
+      jj -= b;
+      ++ii;
+    }
+  }
+  for (int k = lane; k < m - 1; k += 64) {
+    const double e = S[(int64_t)track(k + 1) * ld + track(k)];
+    if (k < a - 1) wa += e;
+    if (k >= a) wb += e;
+  }
+  bet = pb_wave_sum(bet);
+  wa = pb_wave_sum(wa);
+  wb = pb_wave_sum(wb);
+  return bet / (double)ab - (double)m * (wa * inva + wb * invb);
+}
+}  // namespace
+
+template <int MP>
+__global__ void __launch_bounds__(256)
+    k_css_perm_big(const gd_chrom_dev *ch, int nchrom, const double *xbuf, int xstride, const uint8_t *status,
+                   int64_t wtotal, int treshold, int runs, double *pvals, unsigned *wq, double *slab,
+                   int64_t slab_per_wg, int ld) {
+  constexpr int NT = 256, P = PB_P;
+  __shared__ uint16_t s_sig[MP * P]; /* element k of column q at k P + q */
+  __shared__ uint16_t s_F[2][MP];    /* the carried tracks, double-buffered while composing */
+  __shared__ double s_X[2 * MP];
+  __shared__ uint32_t s_mag[MP + 1];
+  __shared__ uint64_t s_st[P + 1];
+  __shared__ int s_hitq[P];
+  __shared__ double s_obs;
+  __shared__ int64_t s_w;
+  __shared__ int s_ctl[3]; /* hits, permutations run, done */
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  double *S = slab + (int64_t)blockIdx.x * slab_per_wg;
+  for (int n = tid; n <= MP; n += NT) s_mag[n] = gd_randint_make(n < 1 ? 1u : (uint32_t)n).magic;
+
+  for (;;) {
+    __syncthreads();
+    if (tid == 0) s_w = (int64_t)atomicAdd(wq, 1u);
+    __syncthreads();
+    const int64_t w = s_w;
+    if (w >= wtotal) break;
+    if (!status[w]) continue;
+    const int c = perm_chrom_of(ch, nchrom, w);
+    const gd_chrom_dev &d = ch[c];
+    const int a = d.asize, b = d.bsize, m = a + b, m1 = m - 1;
+    if (m > MP || m > ld) continue; /* the MDS stage flagged it and wrote no coordinates */
+    const int64_t wl = w - d.w_base;
+    for (int e = tid; e < 2 * m; e += NT) s_X[e] = xbuf[w * xstride + e];
+    for (int i = tid; i < m; i += NT) s_F[0][i] = (uint16_t)i; /* tracks := identity */
+    __syncthreads();
+    /* S = calc_dist(X) (css.c:573-587), symmetric bit for bit */
+    for (int e = tid; e < m * m; e += NT) {
+      const int x = e % m, y = e / m;
+      S[(int64_t)y * ld + x] = x == y ? 0.0 : perm_xdist(s_X, x, y);
+    }
+    __threadfence_block();
+    __syncthreads();
+    const double inva = a > 1 ? 1.0 / (double)(a * a * (a - 1)) : 0.0;
+    const double invb = b > 1 ? 1.0 / (double)(b * b * (b - 1)) : 0.0;
+    if (wave == 0) {
+      const double o = pb_score([](int k) { return k; }, S, ld, a, b, inva, invb, lane);
+      if (lane == 0) s_obs = o;
+    }
+    if (tid == 0) {
+      s_ctl[0] = 0;
+      s_ctl[1] = 0;
+      s_ctl[2] = !(treshold > 0 && runs > 0);
+    }
+    __syncthreads();
+    const double obs = s_obs;
+    uint64_t base = gd_window_state(d.seed, GD_STREAM_CSS, wl);
+    const gd_affine Jq = gd_lcg_jump((uint64_t)lane * (uint64_t)m1), JP = gd_lcg_jump((uint64_t)P * (uint64_t)m1);
+    int cur = 0;
+    while (!s_ctl[2]) {
+      /* 1. draws: wave 0, lane q -> sigma_q in column q */
+      uint16_t *col = s_sig + lane;
+      bool rej = false;
+      if (wave == 0) {
+        for (int k = 0; k < m; ++k) col[k * P] = (uint16_t)k;
+        rej = fy_big_fast(col, gd_affine_apply(Jq, base), m, s_mag);
+      }
+      if (__syncthreads_or(rej)) {
+        if (tid == 0) {
+          uint64_t y = base;
+          for (int q = 0; q < P; ++q) {
+            s_st[q] = y;
+            for (int s2 = 0; s2 < m1; ++s2) {
+              const gd_randint rd = perm_rd((uint32_t)(m - s2), s_mag[m - s2]);
+              do y = gd_lcg_next(y);
+              while (gd_lcg_value(y) > rd.limit);
+            }
+          }
+          s_st[P] = y;
+        }
+        __syncthreads();
+        if (wave == 0) {
+          for (int k = 0; k < m; ++k) col[k * P] = (uint16_t)k;
+          fy_big_exact(col, s_st[lane], m, s_mag);
+        }
+        base = s_st[P];
+      } else {
+        base = gd_affine_apply(JP, base);
+      }
+      __syncthreads();
+      /* 2. compositions F_q = F_{q-1} o sigma_q, F_q over sigma_q */
+      for (int q = 0; q < P; ++q) {
+        for (int i = tid; i < m; i += NT) {
+          const uint16_t v = s_F[cur][s_sig[i * P + q]];
+          s_F[cur ^ 1][i] = v;
+          s_sig[i * P + q] = v;
+        }
+        cur ^= 1;
+        __syncthreads();
+      }
+      /* 3. scores: wave v takes tracks v, v + 4, ... */
+      for (int q = wave; q < P; q += NT / 64) {
+        const double sc = pb_score([&](int k) { return (int)s_sig[k * P + q]; }, S, ld, a, b, inva, invb, lane);
+        if (lane == 0) s_hitq[q] = sc >= obs;
+      }
+      __syncthreads();
+      /* 4. hits in permutation order, early exit at the treshold-th hit */
+      if (tid == 0) {
+        int hits = s_ctl[0], nsc = s_ctl[1];
+        const int valid = min(P, runs - nsc);
+        bool done = false;
+        for (int q = 0; q < valid && !done; ++q) {
+          hits += s_hitq[q];
+          ++nsc;
+          done = hits >= treshold;
+        }
+        s_ctl[0] = hits;
+        s_ctl[1] = nsc;
+        s_ctl[2] = done || nsc >= runs;
+      }
+      __syncthreads();
+    }
+    if (tid == 0) pvals[d.w_out + wl] = (s_ctl[0] + 1) * 1.0 / (s_ctl[1] + 1);
+  }
+}
+
 template <int MP>
 static int launch_perm(const gd_chrom_dev *d_ch, int nchrom, const double *xbuf, const uint8_t *status, int64_t wtotal,
                        int treshold, int runs, double *p, unsigned *wq, hipStream_t s) {
@@ -714,7 +923,7 @@ static int launch_perm(const gd_chrom_dev *d_ch, int nchrom, const double *xbuf,
 }
 
 int gd_css_perm_launch(int mp, const gd_chrom_dev *d_ch, int nchrom, const double *xbuf, const uint8_t *status,
-                       int64_t wtotal, int treshold, int runs, double *p, unsigned *wq, hipStream_t s) {
+                       int64_t wtotal, int treshold, int runs, double *p, unsigned *wq, double *slab, hipStream_t s) {
 #ifdef GD_PERM_PROFILE
   {
     static const unsigned long long z[8] = {0};
@@ -749,6 +958,18 @@ int gd_css_perm_launch(int mp, const gd_chrom_dev *d_ch, int nchrom, const doubl
     case 80: return launch_perm<80>(d_ch, nchrom, xbuf, status, wtotal, treshold, runs, p, wq, s);
     case 96: return launch_perm<96>(d_ch, nchrom, xbuf, status, wtotal, treshold, runs, p, wq, s);
     case 128: return launch_perm<128>(d_ch, nchrom, xbuf, status, wtotal, treshold, runs, p, wq, s);
+  }
+  if (mp > GD_CSS_TIER_MAX && mp <= GD_CSS_BIG_MAX) {
+    const unsigned grid = (unsigned)gd_css_big_grid(wtotal);
+    const int64_t per = gd_css_big_slab_per_wg(mp);
+    const int ld = gd_css_big_ld(mp);
+    if (mp <= 256)
+      hipLaunchKernelGGL(k_css_perm_big<256>, dim3(grid), dim3(256), 0, s, d_ch, nchrom, xbuf, 2 * mp, status, wtotal,
+                         treshold, runs, p, wq, slab, per, ld);
+    else
+      hipLaunchKernelGGL(k_css_perm_big<512>, dim3(grid), dim3(256), 0, s, d_ch, nchrom, xbuf, 2 * mp, status, wtotal,
+                         treshold, runs, p, wq, slab, per, ld);
+    return hipGetLastError() == hipSuccess ? GD_OK : GD_ERR_HIP;
   }
   return GD_ERR_SIZE;
 }

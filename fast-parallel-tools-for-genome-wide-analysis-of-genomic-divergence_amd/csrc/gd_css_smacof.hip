@@ -195,16 +195,25 @@ __global__ void __launch_bounds__(256)
 /* ------------------------------------------------------------------------ */
 /* SMACOF (mds = 1: smacof_runs; mds = 2: one run from the cmds coordinates)   */
 /* ------------------------------------------------------------------------ */
-template <int MP, bool FREQ>
+/* BIG (the general path, m above the register tiers): the counts and the stress triangle
+ * live in the workgroup's global-memory slab (tri first, mpb (mpb - 1) / 2 doubles for the
+ * batch's tier mpb, then the counts at column stride ld) and the workgroups loop over
+ * windows; otherwise both are in LDS, one workgroup per window. */
+template <int MP, bool FREQ, bool BIG>
 __global__ void __launch_bounds__(64 * ((MP + 63) / 64))
     k_css_smacof(const gd_chrom_dev *ch, int nchrom, const gd_css_planes *pl, const uint32_t *planes,
                  const int32_t *lo_a_, const int32_t *hi_a_, const int32_t *lo_b_, const double *avals,
                  const double *bvals, int64_t wtotal, int mds, int want_x, int force_literal, int xstride,
-                 double *scores, double *pvals, double *xbuf, uint8_t *status, unsigned *flags) {
+                 double *scores, double *pvals, double *xbuf, uint8_t *status, unsigned *flags, double *slab,
+                 int64_t slab_per_wg, int mpb, int ld) {
   constexpr int NT = 64 * ((MP + 63) / 64), NW = NT / 64;
   constexpr int NTRI = MP * (MP - 1) / 2;
-  __shared__ uint16_t s_cnt[MP * MP]; /* count D[i][j] at j*MP + i */
-  __shared__ double s_tri[NTRI];      /* stress terms, (i, j < i) at i(i-1)/2 + j */
+  __shared__ uint16_t s_cnt_l[BIG ? 1 : MP * MP]; /* count D[i][j] at j*cs + i */
+  __shared__ double s_tri_l[BIG ? 1 : NTRI];      /* stress terms, (i, j < i) at i(i-1)/2 + j */
+  double *const s_tri = BIG ? slab + (int64_t)blockIdx.x * slab_per_wg : s_tri_l;
+  uint16_t *const s_cnt =
+      BIG ? reinterpret_cast<uint16_t *>(s_tri + (int64_t)mpb * (mpb - 1) / 2 + 8) : s_cnt_l;
+  const int cs = BIG ? ld : MP; /* count column stride */
   __shared__ double s_z[2][2 * MP];   /* configurations, row-major m x 2 */
   __shared__ double s_best[2 * MP];
   __shared__ uint64_t s_mask[2 * MP];
@@ -214,23 +223,23 @@ __global__ void __launch_bounds__(64 * ((MP + 63) / 64))
   __shared__ int s_irr;
 
   const int tid = threadIdx.x;
-  const int64_t w = blockIdx.x;
-  if (w >= wtotal) return;
-  if (mds == 2 && !status[w]) return; /* discarded in the classical stage */
+  for (int64_t w = blockIdx.x; w < wtotal; w += BIG ? (int64_t)gridDim.x : wtotal) {
+  if (BIG) __syncthreads(); /* the previous window's readers are done */
+  if (mds == 2 && !status[w]) continue; /* discarded in the classical stage */
   const int c = sm_chrom_of(ch, nchrom, w);
   const gd_chrom_dev &d = ch[c];
   const int a = d.asize, b = d.bsize, m = a + b;
   const int64_t wl = w - d.w_base;
   const int32_t la = lo_a_[w], ha = hi_a_[w], lb = lo_b_[w];
   const int npos = (ha - la) / a;
-  if (npos <= 0) return;
+  if (npos <= 0) continue;
   if ((int64_t)lb + (int64_t)npos * b > d.blen) {
     if (tid == 0) atomicOr(flags, GD_FLAG_B_BOUNDS);
-    return;
+    continue;
   }
   if (m > MP || (FREQ && (a != 1 || b != 1)) || (!FREQ && npos > 65535)) {
     if (tid == 0) atomicOr(flags, GD_FLAG_BAD_SIZE);
-    return;
+    continue;
   }
   const bool row = tid < m;
 
@@ -245,14 +254,14 @@ __global__ void __launch_bounds__(64 * ((MP + 63) / 64))
     }
     __syncthreads();
     fdel = s_f;
-    if (2 + (fdel < 0.00001 ? 2 : 0) > 2) return;
+    if (2 + (fdel < 0.00001 ? 2 : 0) > 2) continue;
   } else {
     const gd_css_planes P = pl[c];
     const uint32_t *pa = planes + P.pa, *pb = planes + P.pb;
     const int64_t ra = la / a, rb = lb / b;
     bool literal = force_literal || (la % a) != 0 || (lb % b) != 0;
     if (tid == 0) s_irr = 0;
-    for (int e = tid; e < MP * MP; e += NT) s_cnt[e] = 0;
+    for (int e = tid; e < (BIG ? cs * m : MP * MP); e += NT) s_cnt[e] = 0;
     __syncthreads();
     if (!literal) {
       int irr = 0;
@@ -284,7 +293,7 @@ __global__ void __launch_bounds__(64 * ((MP + 63) / 64))
           const uint64_t Pi = s_mask[2 * tid], Ni = s_mask[2 * tid + 1];
           for (int j = 0; j < m; ++j) {
             const uint64_t Pj = s_mask[2 * j], Nj = s_mask[2 * j + 1];
-            s_cnt[j * MP + tid] = (uint16_t)(s_cnt[j * MP + tid] + __popcll(Pi & Nj) + __popcll(Ni & Pj));
+            s_cnt[j * cs + tid] = (uint16_t)(s_cnt[j * cs + tid] + __popcll(Pi & Nj) + __popcll(Ni & Pj));
           }
         }
       }
@@ -303,7 +312,7 @@ __global__ void __launch_bounds__(64 * ((MP + 63) / 64))
              * and the A element across populations (css.c:281-326) */
             const bool cast_i = ((tid < a) == (j < a)) ? (tid > j) : (tid < a);
             const double prod = cast_i ? sm_x86_int(vi) * vj : sm_x86_int(vj) * vi;
-            if (prod == -9.0) s_cnt[j * MP + tid] = (uint16_t)(s_cnt[j * MP + tid] + 1);
+            if (prod == -9.0) s_cnt[j * cs + tid] = (uint16_t)(s_cnt[j * cs + tid] + 1);
           }
         }
       }
@@ -313,7 +322,7 @@ __global__ void __launch_bounds__(64 * ((MP + 63) / 64))
     double unv = 0.0, sum = 0.0;
     if (row)
       for (int j = 0; j < m; ++j) {
-        const int cj = s_cnt[j * MP + tid];
+        const int cj = s_cnt[j * cs + tid];
         if (cj == 0)
           unv += 1.0;
         else
@@ -336,7 +345,7 @@ __global__ void __launch_bounds__(64 * ((MP + 63) / 64))
       sum += s_red[NW + k];
     }
     const int tot = m * m;
-    if ((int)unv > tot / 2) return; /* discarded window: outputs untouched */
+    if ((int)unv > tot / 2) continue; /* discarded window: outputs untouched */
     avg = sum / tot;
   }
   /* delta(i, j), i != j */
@@ -346,7 +355,7 @@ __global__ void __launch_bounds__(64 * ((MP + 63) / 64))
       (void)j;
       return fdel;
     } else {
-      const int cij = s_cnt[j * MP + i];
+      const int cij = s_cnt[j * cs + i];
       return cij == 0 ? avg : (double)cij;
     }
   };
@@ -462,7 +471,7 @@ __global__ void __launch_bounds__(64 * ((MP + 63) / 64))
   const double score = s_sig;
   if (score == -1.0) { /* the reference's "discarded" marker (css.c:127) */
     if (tid == 0 && want_x) status[w] = 0;
-    return;
+    continue;
   }
   if (tid == 0) {
     scores[d.w_out + wl] = score;
@@ -472,16 +481,20 @@ __global__ void __launch_bounds__(64 * ((MP + 63) / 64))
     for (int e = tid; e < xstride; e += NT) xbuf[w * xstride + e] = (e < 2 * m) ? Xf[e] : 0.0;
     if (tid == 0) status[w] = 1;
   }
+  }
 }
 
-template <int MP, bool FREQ>
+template <int MP, bool FREQ, bool BIG = false>
 static int launch_smacof(const gd_chrom_dev *d_ch, int nchrom, const gd_css_planes *d_pl, const uint32_t *planes,
                          const int32_t *lo_a, const int32_t *hi_a, const int32_t *lo_b, const double *avals,
                          const double *bvals, int64_t wtotal, int mds, int want_x, int force_literal, int xstride,
-                         double *scores, double *p, double *xbuf, uint8_t *status, unsigned *flags, hipStream_t s) {
-  hipLaunchKernelGGL((k_css_smacof<MP, FREQ>), dim3((unsigned)wtotal), dim3(64 * ((MP + 63) / 64)), 0, s, d_ch,
+                         double *scores, double *p, double *xbuf, uint8_t *status, unsigned *flags, hipStream_t s,
+                         double *slab = nullptr, int mpb = 0) {
+  const int64_t grid = BIG ? gd_css_big_grid(wtotal) : wtotal;
+  hipLaunchKernelGGL((k_css_smacof<MP, FREQ, BIG>), dim3((unsigned)grid), dim3(64 * ((MP + 63) / 64)), 0, s, d_ch,
                      nchrom, d_pl, planes, lo_a, hi_a, lo_b, avals, bvals, wtotal, mds, want_x, force_literal,
-                     xstride, scores, p, xbuf, status, flags);
+                     xstride, scores, p, xbuf, status, flags, slab, BIG ? gd_css_big_slab_per_wg(mpb) : 0, mpb,
+                     BIG ? gd_css_big_ld(mpb) : 0);
   return hipGetLastError() == hipSuccess ? GD_OK : GD_ERR_HIP;
 }
 
@@ -490,7 +503,7 @@ int gd_css_smacof_launch(int mp, bool freq, const gd_chrom_dev *d_ch, int nchrom
                          const uint32_t *planes, const int32_t *lo_a, const int32_t *hi_a, const int32_t *lo_b,
                          const double *avals, const double *bvals, int64_t wtotal, int mds, int want_x,
                          int force_literal, double *scores, double *p, double *xbuf, uint8_t *status,
-                         unsigned *flags, hipStream_t s) {
+                         unsigned *flags, double *slab, hipStream_t s) {
   const int xs = 2 * mp;
 #define SM_CASE(T)                                                                                          \
   case T:                                                                                                   \
@@ -506,6 +519,13 @@ int gd_css_smacof_launch(int mp, bool freq, const gd_chrom_dev *d_ch, int nchrom
     SM_CASE(80)
     SM_CASE(96)
     SM_CASE(128)
+    default:
+      if (mp > GD_CSS_TIER_MAX && mp <= 256)
+        return launch_smacof<256, false, true>(d_ch, nchrom, d_pl, planes, lo_a, hi_a, lo_b, avals, bvals, wtotal, mds,
+                                               want_x, force_literal, xs, scores, p, xbuf, status, flags, s, slab, mp);
+      if (mp > 256 && mp <= GD_CSS_BIG_MAX)
+        return launch_smacof<512, false, true>(d_ch, nchrom, d_pl, planes, lo_a, hi_a, lo_b, avals, bvals, wtotal, mds,
+                                               want_x, force_literal, xs, scores, p, xbuf, status, flags, s, slab, mp);
   }
 #undef SM_CASE
   return GD_ERR_SIZE;

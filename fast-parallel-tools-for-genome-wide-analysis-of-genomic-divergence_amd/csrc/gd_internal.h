@@ -38,6 +38,23 @@ typedef struct gd_chrom_dev {
 #define GD_LUT_CAP (1 << 22) /* FET score-table entries (32 MB): up to ~62+62 individuals */
 #define GD_NREP 100 /* bootstrap replicates (cFisher.c:62) */
 
+/* CSS cohort sizes (m = asize + bsize): register tiers up to GD_CSS_TIER_MAX; the general
+ * path (k_css_mds_big, k_css_perm_big, k_css_smacof_big) above, up to GD_CSS_BIG_MAX, with
+ * each workgroup's matrices in a global-memory slab of its own (L2 / Infinity-Cache resident) */
+#define GD_CSS_TIER_MAX 128
+#define GD_CSS_BIG_MAX 512
+#define GD_CSS_BIG_GRID 1024 /* workgroups = slabs of the general-path kernels */
+/* leading dimension (doubles) of a general-path matrix: m rounded up to 128-byte columns */
+static inline int gd_css_big_ld(int m) { return (m + 15) & ~15; }
+/* doubles of one workgroup's slab: the m x ld matrix of the MDS / permutation kernels or
+ * SMACOF's 16-bit counts + packed stress triangle, whichever is larger */
+static inline int64_t gd_css_big_slab_per_wg(int m) {
+  const int64_t mds = (int64_t)gd_css_big_ld(m) * m;
+  const int64_t sm = (int64_t)m * (m - 1) / 2 + 8 + ((int64_t)gd_css_big_ld(m) * m + 3) / 4 + 8;
+  return (mds > sm ? mds : sm) + 32;
+}
+static inline int64_t gd_css_big_grid(int64_t wtotal) { return wtotal < GD_CSS_BIG_GRID ? wtotal : GD_CSS_BIG_GRID; }
+
 /* CSS bit planes of one chromosome (word offsets into the plane buffer).  Pop A:
  * individual i's "== 3" plane at pa + 2i*wa, its "== -3" plane at pa + (2i+1)*wa,
  * the per-row "irregular value" plane at pa + 2*asize*wa; pop B likewise.  A plane

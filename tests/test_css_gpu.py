@@ -113,11 +113,14 @@ def test_reference_entry_point_in_place(oracle):
     assert np.all(p[s_ref == 0] == -7.0)  # untouched at uncomputed windows
 
 
-def test_cohort_above_largest_tier_raises():
-    from gdscan import GdError, css
-    av, bv, ap, bp, regend = _synth(10, 2_000, 70, 70)
-    with pytest.raises(GdError):
-        css.scan(av, bv, ap, bp, regend)
+def test_cohort_above_largest_tier_takes_the_general_path(oracle):
+    """70 + 70 individuals: above the register tiers, scored by k_css_mds_big
+    (tests/test_css_big.py covers that path in depth)."""
+    from gdscan import css
+    av, bv, ap, bp, regend = _synth(10, 1_100, 70, 70)
+    s, p = css.scan(av, bv, ap, bp, regend)
+    s_ref, p_ref = oracle_css_scan(oracle, av, bv, ap, bp, regend)
+    _cmp_scores(s, s_ref)
 
 
 def test_device_batch_api_matches_host(oracle):
