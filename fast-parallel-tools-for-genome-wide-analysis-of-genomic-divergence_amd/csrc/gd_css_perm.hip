@@ -76,6 +76,10 @@ __device__ __forceinline__ double perm_xdist(const double *X, int i, int j) {
   return sqrt(dx * dx + dy * dy);
 }
 
+#ifndef PERM_MFMA
+#define PERM_MFMA 1 /* the permutation score on the matrix cores up to 80 individuals */
+#endif
+
 /* Row stride of the byte matrices: row k holds byte k of every lane's column.  68
  * bytes (17 dwords, odd) put the 64 rows a composition step writes, one per lane,
  * on distinct LDS banks; 64 bytes put them all on two. */
@@ -93,12 +97,23 @@ struct PermShape {
   static constexpr int NT = 64 * NWV;
   static constexpr int SIG = MP * PERM_ROW; /* one wave's byte matrix */
   static constexpr int MEM = HALF * 64;     /* one wave's member lists (byte k of lane l at k*64 + l) */
-  /* region U: the FP64 triangle while a window is set up, then the FP32 triangle, the
-   * byte matrices and the member lists */
-  static constexpr int OFF_SIG = (TRI * 4 + 15) / 16 * 16;
+  /* The matrix-core score (score_mfma) for cohorts up to 80: S scaled by a power of two
+   * into one fp16 matrix, MT 32-row tiles x KT 16-deep k steps of v_mfma_f32_32x32x16_f16;
+   * row stride RS bytes,
+   * an odd multiple of 16, so the 16-byte A-fragment reads of 16 consecutive rows hit
+   * distinct bank groups */
+  static constexpr bool MF = PERM_MFMA && MP <= 80;
+  static constexpr int MT = (MP + 31) / 32, KT = (MP + 15) / 16;
+  static constexpr int RS = KT * 32 + 16;
+  static constexpr int S16 = MT * 32 * RS; /* bytes of the fp16 matrix */
+  /* region U: the FP64 triangle while a window is set up; then either the FP32 triangle,
+   * the byte matrices and the member lists (FP32 score), or the fp16 matrix,
+   * the byte matrices and the serial-stream start states (matrix-core score) */
+  static constexpr int OFF_SIG = MF ? S16 : (TRI * 4 + 15) / 16 * 16;
   static constexpr int OFF_MEM = OFF_SIG + NWV * SIG;
-  static constexpr int UBYTES = OFF_MEM + NWV * MEM > TRI * 8 ? OFF_MEM + NWV * MEM : TRI * 8;
-  static_assert(NWV * MEM >= (NT + 1) * 8, "the serial-stream start states alias the member lists");
+  static constexpr int MEMB = MF ? (NT + 1) * 8 : NWV * MEM;
+  static constexpr int UBYTES = OFF_MEM + MEMB > TRI * 8 ? OFF_MEM + MEMB : TRI * 8;
+  static_assert(MEMB >= (NT + 1) * 8, "the serial-stream start states alias the member lists");
 };
 
 /* packed lower triangle with one zero row appended: pair (x, y), x != y, at
@@ -352,6 +367,154 @@ __device__ __forceinline__ void score_f32(const float *S32, const double *R, con
   err = 2.0 * eq / ab + apb * (ewa * inva + ewb * invb) + 1e-11 * mag;
 }
 
+typedef _Float16 pm_f16x8 __attribute__((ext_vector_type(8)));
+typedef float pm_f32x16 __attribute__((ext_vector_type(16)));
+
+/* index of the k-th set bit of (lo, hi), k < popcount */
+__device__ __forceinline__ uint32_t pm_kth_bit(uint64_t lo, uint64_t hi, int k) {
+  const int c = __popcll(lo);
+  uint64_t x = lo;
+  uint32_t base = 0;
+  if (k >= c) {
+    k -= c;
+    x = hi;
+    base = 64;
+  }
+  while (k-- > 0) x &= x - 1;
+  return base + (uint32_t)__builtin_ctzll(x);
+}
+
+/* The score of every lane's track on the matrix cores (the between-group sum of
+ * css.c:608-647 as a bilinear form).  With x_p the indicator of group A under
+ * permutation p, bet_p = sum_{i in A, j in B} S_ij = x_p^T S (1 - x_p): one wave forms
+ * Y = S (1 - X) for its 64 permutations (X: individuals x permutations, 0/1, exact in
+ * fp16) as v_mfma_f32_32x32x16_f16 products with S scaled by a power of two sc (its
+ * largest entry to [2^14, 2^15)) and rounded to fp16, then bet_p = sum_i X_ip Y_ip from
+ * the accumulator tiles (lane l holds column l & 31, rows (reg & 3) + 8 (reg >> 2) +
+ * 4 (l >> 5) of each 32 x 32 tile).  The consecutive within-group pairs (Q8) are gathered
+ * from the same matrix.  Error bound, u = 2^-24: an entry is within 2^-10 of its scaled
+ * value plus 2^-25 absolute (fp16 subnormals; a float rounding first); the products with
+ * 0/1 are exact; each Y entry takes <= 16 KT fp32 roundings and each dot <= 32 MT + 1
+ * more, so |bet - est| <= (2^-10 + u (16 KT + 32 MT + 4)) bet + a b 2^-25 / sc; the pair
+ * sums likewise with their term counts.  est and err as score_f32: |score_exact - est|
+ * <= err, and the few lanes inside the bound recompute in FP64.  Also returns the lane's
+ * group-A membership (alo, ahi). */
+template <int MP>
+__device__ __forceinline__ void score_mfma(const char *s16, const uint2 *lut, const uint8_t *col, const uint8_t *fmap,
+                                           bool mapped, int a, int b, double inva, double invb, double inv_sc,
+                                           int lane, double &est, double &err, uint64_t &alo, uint64_t &ahi) {
+  using SH = PermShape<MP>;
+  constexpr int MT = SH::MT, KT = SH::KT, RS = SH::RS;
+  const int m = a + b;
+  auto track = [&](int k) -> uint32_t {
+    const uint32_t c = col[k * PERM_ROW];
+    return mapped ? (uint32_t)fmap[c] : c;
+  };
+  auto s_at = [&](uint32_t x, uint32_t y) -> float {
+    return (float)*reinterpret_cast<const _Float16 *>(s16 + x * RS + 2 * y);
+  };
+  /* group A's members and the consecutive pairs */
+  uint64_t lo = 0, hi = 0;
+  auto add = [&](uint32_t x) {
+    lo |= x < 64 ? 1ull << (x & 63u) : 0ull;
+    if constexpr (MP > 64) hi |= x >= 64 ? 1ull << (x & 63u) : 0ull;
+  };
+  float wa = 0.f, wb = 0.f;
+  uint32_t prev = track(0);
+  if (a > 0) add(prev);
+#pragma unroll 4
+  for (int k = 1; k < a; ++k) {
+    const uint32_t cur = track(k);
+    wa += s_at(prev, cur);
+    add(cur);
+    prev = cur;
+  }
+  if (a < m) prev = track(a);
+#pragma unroll 4
+  for (int k = a + 1; k < m; ++k) {
+    const uint32_t cur = track(k);
+    wb += s_at(prev, cur);
+    prev = cur;
+  }
+  alo = lo;
+  ahi = hi;
+  const uint64_t vlo = m >= 64 ? ~0ull : ((1ull << m) - 1), vhi = m > 64 ? ((1ull << (m - 64)) - 1) : 0ull;
+  const uint64_t clo = ~lo & vlo, chi = ~hi & vhi; /* group B = the complement within m */
+  /* the masks of the two permutations whose columns this lane's fragments carry */
+  const int r = lane & 31, h = lane >> 5;
+  auto pull = [](uint64_t v, int src) -> uint64_t {
+    const uint32_t l = (uint32_t)__builtin_amdgcn_ds_bpermute(src << 2, (int)(uint32_t)v);
+    const uint32_t u = (uint32_t)__builtin_amdgcn_ds_bpermute(src << 2, (int)(uint32_t)(v >> 32));
+    return ((uint64_t)u << 32) | l;
+  };
+  uint64_t cm[2][2], am[2][2];
+  cm[0][0] = pull(clo, r);
+  cm[1][0] = pull(clo, 32 + r);
+  am[0][0] = pull(lo, r);
+  am[1][0] = pull(lo, 32 + r);
+  if constexpr (MP > 64) {
+    cm[0][1] = pull(chi, r);
+    cm[1][1] = pull(chi, 32 + r);
+    am[0][1] = pull(hi, r);
+    am[1][1] = pull(hi, 32 + r);
+  } else {
+    cm[0][1] = cm[1][1] = am[0][1] = am[1][1] = 0;
+  }
+  /* one 32 x 32 output tile at a time (16 accumulators live): for each column tile n and
+   * row tile t, the k steps accumulate, then the tile's rows of this lane's column enter
+   * the dot with X */
+  float own = 0.f, send = 0.f;
+#pragma unroll 1
+  for (int n = 0; n < 2; ++n) {
+    const uint64_t c0 = n ? cm[1][0] : cm[0][0], c1 = n ? cm[1][1] : cm[0][1];
+    const uint64_t a0 = n ? am[1][0] : am[0][0], a1 = n ? am[1][1] : am[0][1];
+    float part = 0.f;
+#pragma unroll 1
+    for (int t = 0; t < MT; ++t) {
+      pm_f32x16 acc;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+#pragma unroll
+      for (int kt = 0; kt < KT; ++kt) {
+        const int k0 = kt * 16 + 8 * h; /* this lane's 8 k of the step */
+        const uint64_t c = k0 < 64 ? c0 >> k0 : c1 >> (k0 - 64);
+        const uint2 l4 = lut[c & 15u], h4 = lut[(c >> 4) & 15u];
+        uint4 v;
+        v.x = l4.x;
+        v.y = l4.y;
+        v.z = h4.x;
+        v.w = h4.y;
+        const pm_f16x8 bf = __builtin_bit_cast(pm_f16x8, v);
+        const pm_f16x8 ah =
+            __builtin_bit_cast(pm_f16x8, *reinterpret_cast<const uint4 *>(s16 + (t * 32 + r) * RS + 2 * k0));
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bf, acc, 0, 0, 0);
+        if (kt & 1) asm volatile("" ::: "memory"); /* two k steps of fragment loads in flight */
+      }
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int i = t * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+        const uint64_t mk = i < 64 ? a0 >> i : a1 >> (i - 64);
+        part += (mk & 1u) ? acc[e] : 0.f;
+      }
+    }
+    if (n == h)
+      own = part;
+    else
+      send = part;
+  }
+  /* the other row half of this lane's column comes from lane ^ 32 */
+  const float q = own + __shfl_xor(send, 32);
+  const double ab = (double)(a * b), apb = (double)(a + b);
+  const double dq = (double)q * inv_sc, dwa = (double)wa * inv_sc, dwb = (double)wb * inv_sc;
+  est = dq / ab - apb * (dwa * inva + dwb * invb);
+  constexpr double U = 0x1p-24, REP = 0x1p-10, SUB = 0x1p-25;
+  const double ebet = (REP + U * (16 * KT + 32 * MT + 4)) * dq * 1.001 + SUB * ab * inv_sc;
+  const double ewa = (REP + U * (a + 4)) * dwa * 1.001 + SUB * a * inv_sc;
+  const double ewb = (REP + U * (b + 4)) * dwb * 1.001 + SUB * b * inv_sc;
+  const double mag = dq / ab + apb * (dwa * inva + dwb * invb);
+  err = ebet / ab + apb * (ewa * inva + ewb * invb) + 1e-11 * mag;
+}
+
 /* every lane's column of one wave's byte matrix := identity (rows k < m; row k is
  * 64 bytes of k) */
 __device__ __forceinline__ void sig_identity(uint8_t *sig, int m, int lane) {
@@ -445,6 +608,12 @@ __global__ void __launch_bounds__(PermShape<MP>::NT) PERM_WPE
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   __shared__ uint32_t s_mag[MP + 1]; /* random_int_nrand48 magic numbers (perm_rd) */
   for (int n = tid; n <= MP; n += NT) s_mag[n] = gd_randint_make(n < 1 ? 1u : (uint32_t)n).magic;
+  __shared__ uint2 s_lut[16]; /* 4 indicator bits -> 4 bf16 (0 or 1.0): score_mfma's B fragments */
+  if (tid < 16) /* fp16 1.0 = 0x3C00 */
+    s_lut[tid] = make_uint2((tid & 1 ? 0x3C00u : 0u) | (tid & 2 ? 0x3C000000u : 0u),
+                            (tid & 4 ? 0x3C00u : 0u) | (tid & 8 ? 0x3C000000u : 0u));
+  const char *s16 = s_U; /* score_mfma: the scaled fp16 matrix */
+  __shared__ unsigned long long s_smax; /* largest S entry of the window (bits of a non-negative double) */
   uint8_t *my_sig = reinterpret_cast<uint8_t *>(s_U + SH::OFF_SIG) + wave * SIG;
   uint8_t *my_mem = reinterpret_cast<uint8_t *>(s_U + SH::OFF_MEM) + wave * SH::MEM;
 
@@ -465,10 +634,12 @@ __global__ void __launch_bounds__(PermShape<MP>::NT) PERM_WPE
     int ln = tid;
     PERM_OPAQUE(ln);
     for (int e = ln; e < 2 * m; e += NT) s_X[e] = xbuf[w * 2 * MP + e];
+    if (tid == 0) s_smax = 0ull;
     __syncthreads();
     /* entry e = T(h) + l of the triangle, e strided over the threads (independent
      * entries, no per-row loop): h from the float root of 8e + 1 (within one of the
      * true row for e < 2^24), then corrected */
+    double vmax = 0.0;
 #pragma unroll 4
     for (int e = ln; e < TRI - 1; e += NT) {
       int h = (int)((1.0f + __fsqrt_rn(8.0f * (float)e + 1.0f)) * 0.5f);
@@ -477,9 +648,16 @@ __global__ void __launch_bounds__(PermShape<MP>::NT) PERM_WPE
       else if (h * (h + 1) / 2 <= e)
         ++h;
       const int l = e - h * (h - 1) / 2;
-      s_S[e] = (h < m && l < m) ? perm_xdist(s_X, h, l) : 0.0;
+      const double v = (h < m && l < m) ? perm_xdist(s_X, h, l) : 0.0;
+      s_S[e] = v;
+      vmax = fmax(vmax, v);
     }
     if (tid == 0) s_S[TRI - 1] = 0.0;
+    if constexpr (SH::MF) { /* the window's largest S entry (v >= 0: the bits order as the values) */
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) vmax = fmax(vmax, __shfl_xor(vmax, o));
+      if (lane == 0 && vmax > 0.0) atomicMax(&s_smax, (unsigned long long)__double_as_longlong(vmax));
+    }
     __syncthreads();
     for (int r = ln; r <= MP; r += NT) {
       double acc = 0.0;
@@ -515,6 +693,32 @@ __global__ void __launch_bounds__(PermShape<MP>::NT) PERM_WPE
           return *reinterpret_cast<const double *>(reinterpret_cast<const char *>(s_S) + tri8(y) + (x << 3));
         },
         s_R, a, b, inva, invb);
+    double inv_sc = 1.0; /* score_mfma: S was scaled by 1 / inv_sc */
+    if constexpr (SH::MF) {
+      /* the scaled fp16 matrix of S over region U (the FP64 triangle is dead once every
+       * thread has its obs): entry (row, k) from the coordinates, the same value the
+       * triangle held, times 2^(15 - e) for the largest entry's binary exponent e; zero
+       * outside m x m and on the diagonal */
+      const double smax = __longlong_as_double((long long)s_smax);
+      int ex = 0;
+      if (smax > 0.0) (void)frexp(smax, &ex);
+      const double sc = ldexp(1.0, 15 - ex);
+      inv_sc = ldexp(1.0, ex - 15);
+      __syncthreads();
+      /* in FP32 (fp16 keeps 11 bits: the FP32 distance's ~2^-22 is inside the bound) */
+      const float scf = (float)sc;
+      constexpr int KC = SH::KT * 16;
+      for (int e = ln; e < SH::MT * 32 * KC; e += NT) {
+        const int row = e / KC, k = e - row * KC;
+        float v = 0.f;
+        if (row < m && k < m && row != k) {
+          const float dx = (float)(s_X[2 * row] - s_X[2 * k]), dy = (float)(s_X[2 * row + 1] - s_X[2 * k + 1]);
+          v = __fsqrt_rn(dx * dx + dy * dy) * scf;
+        }
+        *reinterpret_cast<_Float16 *>(s_U + row * SH::RS + 2 * k) = (_Float16)v;
+      }
+      __syncthreads();
+    } else
     /* FP32 copy of the triangle over the head of the FP64 one, in chunks (the FP32
      * entries of chunk j overlap only FP64 entries of chunks <= j, read before) */
     {
@@ -650,7 +854,16 @@ __global__ void __launch_bounds__(PermShape<MP>::NT) PERM_WPE
       double est, err;
       const bool mapped = __builtin_amdgcn_readfirstlane(wave) > 0;
       const uint8_t *fmap = s_fs + __builtin_amdgcn_readfirstlane(wave) * MP;
-      score_f32<MP>(s_S32, s_R, tcol, fmap, mapped, mcol, a, b, inva, invb, est, err);
+      uint64_t glo = 0, ghi = 0; /* the smaller group's members (score_mfma) */
+      if constexpr (SH::MF) {
+        uint64_t alo, ahi;
+        score_mfma<MP>(s16, s_lut, tcol, fmap, mapped, a, b, inva, invb, inv_sc, lane, est, err, alo, ahi);
+        const uint64_t vlo = m >= 64 ? ~0ull : ((1ull << m) - 1), vhi = m > 64 ? ((1ull << (m - 64)) - 1) : 0ull;
+        glo = a <= b ? alo : ~alo & vlo;
+        ghi = a <= b ? ahi : ~ahi & vhi;
+      } else {
+        score_f32<MP>(s_S32, s_R, tcol, fmap, mapped, mcol, a, b, inva, invb, est, err);
+      }
       if (force_exact) err = __builtin_inf();
       int hit = est - obs > err ? 1 : (obs - est > err ? 0 : -1);
 #ifdef PERM_COUNT_AMBIGUOUS /* diagnostics: ambiguous lanes and wave-passes that ran the FP64 path */
@@ -664,7 +877,12 @@ __global__ void __launch_bounds__(PermShape<MP>::NT) PERM_WPE
                 const uint32_t c = tcol[k * PERM_ROW];
                 return mapped ? (uint32_t)fmap[c] : c;
               },
-              [&](int k) { return k < g ? (uint32_t)mcol[k * 64] : (uint32_t)MP; },
+              [&](int k) {
+                if constexpr (SH::MF)
+                  return k < g ? pm_kth_bit(glo, ghi, k) : (uint32_t)MP;
+                else
+                  return k < g ? (uint32_t)mcol[k * 64] : (uint32_t)MP;
+              },
               [&](uint32_t x, uint32_t y) { return y < (uint32_t)m ? perm_xdist(s_X, (int)y, (int)x) : 0.0; }, s_R,
               a, b, inva, invb);
           hit = sc >= obs;

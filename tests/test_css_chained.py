@@ -72,7 +72,7 @@ def test_chained_convention_matches_per_window_oracle(oracle, a, b, treshold, ru
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("a,b,treshold,runs,nsnp", [(20, 20, 50, 400, 15_000), (40, 40, 10, 1000, 4_000)])
+@pytest.mark.parametrize("a,b,treshold,runs,nsnp", [(20, 20, 50, 400, 15_000), (12, 13, 30, 300, 15_000)])
 def test_chained_convention_matches_gpu(oracle, a, b, treshold, runs, nsnp):
     from gdscan import css, synth
     av, bv, ap, bp, regend = synth.chromosome(71, nsnp, a, b)

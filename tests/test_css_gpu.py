@@ -259,12 +259,17 @@ def test_serial_window_set_with_permutations(oracle):
 @pytest.mark.parametrize("asize,bsize,treshold,runs,nsnp,dup", [(10, 10, 100_000, 500, 15_000, False),
                                                                 (40, 40, 100_000, 300, 3_000, False),
                                                                 (6, 9, 100_000, 1000, 10_000, True),
-                                                                (40, 40, 10, 1000, 3_000, True)])
+                                                                (40, 40, 10, 1000, 3_000, True),
+                                                                (20, 20, 100_000, 400, 6_000, True),
+                                                                (45, 45, 100_000, 200, 1_800, False),
+                                                                (64, 64, 100_000, 100, 1_400, True)])
 def test_fp32_prefilter_changes_no_p(asize, bsize, treshold, runs, nsnp, dup, monkeypatch):
-    """The permutation kernel decides hits from the FP32 copy of S and recomputes in
-    FP64 only where the estimate is within its error bound of the observed score;
-    GD_PERM_EXACT=1 scores every permutation in FP64.  The p-values must be identical,
-    including windows full of exact ties (duplicated individuals)."""
+    """The permutation kernel decides hits from an estimate -- the matrix-core score
+    (score_mfma, fp16 S on v_mfma_f32_32x32x16_f16) up to 80 individuals, the FP32 copy of
+    S above -- and recomputes in FP64 only where the estimate is within its error bound
+    of the observed score; GD_PERM_EXACT=1 scores every permutation in FP64.  The
+    p-values must be identical, including windows full of exact ties (duplicated
+    individuals), at the MFMA tiers (24, 40, 80) and the FP32 tiers (96, 128)."""
     from gdscan import css
     av, bv, ap, bp, regend = _synth(8, nsnp, asize, bsize)
     if dup:
