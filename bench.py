@@ -666,6 +666,16 @@ def c45_leg(env, args, name, treshold, runs, queue):
         pv_ = css_valu("c5_perm", mine_w, float(stage[1]))
         if pv_:
             out["permutations"]["valu"] = pv_
+        doc = json.loads(CSS_VALU_FILE.read_text()).get("c5_perm", {}) if CSS_VALU_FILE.exists() else {}
+        if "mfma" in doc and stage[1] > 0:
+            # matrix-core share of the permutation kernel (score_mfma): MFMA busy SIMD-cycles per
+            # window (committed PMC profile) x this rank's windows over its SIMD-cycles at 2.4 GHz
+            mf = doc["mfma"]
+            busy = mf["busy_simd_cycles_per_dispatch"] / doc["windows_per_dispatch"] * mine_w
+            out["permutations"]["mfma"] = {
+                "instruction": "v_mfma_f32_32x32x16_f16", "busy_frac": busy / (1024 * 2.4e9 * stage[1] * 1e-3),
+                "mfma_per_window": mf["mfma_per_dispatch"] / doc["windows_per_dispatch"],
+                "source": f"{CSS_VALU_FILE.relative_to(ROOT)} [c5_perm.mfma] ({mf['method']})"}
     if env.rank == 0 and env.world == 1 and not args.no_cpu:
         out["cpu_baseline"] = css_cpu_baseline(args, pop, treshold, runs)
     del av, bv, ap, bp

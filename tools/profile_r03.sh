@@ -27,5 +27,8 @@ timeout -s KILL 200 rocprofv3 --pmc $SQ -d $O/pmc_c3 -o run --output-format csv 
 POP=40 NCH=4 RUNS=0 STEPS=1 timeout -s KILL 200 rocprofv3 --pmc $SQ -d $O/pmc_c4 -o run --output-format csv -- \
     python3 tools/css_time.py > $O/pmc_c4.txt 2> $O/pmc_c4.err &&
 POP=40 NCH=1 RUNS=1000 TRES=10 STEPS=1 timeout -s KILL 200 rocprofv3 --pmc $SQ -d $O/pmc_c5 -o run \
-    --output-format csv -- python3 tools/css_time.py > $O/pmc_c5.txt 2> $O/pmc_c5.err
+    --output-format csv -- python3 tools/css_time.py > $O/pmc_c5.txt 2> $O/pmc_c5.err &&
+POP=40 NCH=1 RUNS=1000 TRES=10 STEPS=1 timeout -s KILL 200 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES \
+    GRBM_GUI_ACTIVE SQ_WAVES -d $O/pmc_c5_mfma -o run --output-format csv -- python3 tools/css_time.py \
+    > $O/pmc_c5_mfma.txt 2> $O/pmc_c5_mfma.err
 echo "profile_r03 exit $?"

@@ -152,6 +152,20 @@ css_entry("c4", src / "pmc_c4", ["k_css_pack", "k_css_mds_t80"], c4t["windows_pe
 c5t = last_json(src / "pmc_c5.txt")
 css_entry("c5_perm", src / "pmc_c5", ["k_css_perm<80>"], c5t["windows_per_scan"],
           "tools/css_time.py: 1 x 500k SNPs, 40+40, mcT=10, mcR=1000")
+# matrix-core share of the permutation kernel (score_mfma): SQ_VALU_MFMA_BUSY_CYCLES counts
+# busy SIMD cycles (32 per v_mfma_f32_32x32x16), GRBM_GUI_ACTIVE the GPU cycles summed over
+# the 8 XCDs
+if (src / "pmc_c5_mfma").exists():
+    mf, nmf = counters(src / "pmc_c5_mfma")
+    need(mf, ["k_css_perm<80>"], "pmc_c5_mfma")
+    k = mf["k_css_perm<80>"]
+    nd = nmf["k_css_perm<80>"]
+    busy, active = k["SQ_VALU_MFMA_BUSY_CYCLES"] / nd, k["GRBM_GUI_ACTIVE"] / nd / 8
+    css_doc["c5_perm"]["mfma"] = {
+        "busy_simd_cycles_per_dispatch": busy, "kernel_cycles": active, "mfma_per_dispatch": busy / 32,
+        "frac": busy / (1024 * active),
+        "method": "rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_WAVES over "
+                  "k_css_perm<80> (tools/css_time.py C5 shape); frac = busy / (1024 SIMDs x GRBM_GUI_ACTIVE / 8)"}
 (dst / f"{R}_css_valu.json").write_text(json.dumps(css_doc, indent=1) + "\n")
 
 # ---- summary
@@ -176,7 +190,9 @@ lines += ["", f"VALU issue peak (ubench, median of simple ops): {peak:.0f} G wav
           "measured issue peak.", ""]
 for k, v in css_doc.items():
     lines.append(f"CSS {k}: {v['valu_wave_insts_per_window']:.0f} VALU wave-instructions per window "
-                 f"({' + '.join(v['kernels'])}).")
+                 f"({' + '.join(v['kernels'])})."
+                 + (f" Matrix cores: {v['mfma']['mfma_per_dispatch'] / 1e6:.1f} M v_mfma_f32_32x32x16_f16 per "
+                    f"dispatch, {100 * v['mfma']['frac']:.1f} % of the SIMD-cycles busy." if "mfma" in v else ""))
 lines += ["", "Bench line (same call):", "", "```", json.dumps(bench), "```"]
 (dst / f"{R}_summary.md").write_text("\n".join(lines) + "\n")
 print("\n".join(lines[:60]))
