@@ -15,21 +15,22 @@ from test_css_perm_isolated import _oracle_p
 pytestmark = pytest.mark.gpu
 
 
-def _cmp(s, s_ref):
+def _cmp(s, s_ref, min_windows=20):
     assert np.array_equal(s == 0, s_ref == 0), "computed-window sets differ"
-    assert (s_ref != 0).sum() >= 20
+    assert (s_ref != 0).sum() >= min_windows
     ok = np.isnan(s_ref) | (np.abs(s - s_ref) <= 1e-9 * np.abs(s_ref) + 1e-12)
     assert ok.all(), (np.flatnonzero(~ok)[:10], s[~ok][:5], s_ref[~ok][:5])
 
 
-@pytest.mark.parametrize("a,b,nsnp", [(70, 70, 500), (100, 100, 400), (129, 3, 500), (150, 120, 300)])
+@pytest.mark.parametrize("a,b,nsnp", [(70, 70, 500), (100, 100, 400), (129, 3, 500), (150, 120, 300),
+                                      (140, 120, 120)])
 def test_general_path_scores(oracle, a, b, nsnp):
     from gdscan import css, synth
     av, bv, ap, bp, regend = synth.chromosome(200 + a, nsnp, a, b)
     s, p = css.scan(av, bv, ap, bp, regend, runs=0, serial=True)
     s_ref, _ = oracle_css_scan(oracle, av, bv, ap, bp, regend, runs=0, serial=True)
-    _cmp(s, s_ref)
-    assert np.all(p[s != 0] == 1.0)
+    _cmp(s, s_ref, 20 if nsnp > 200 else 6)  # 257..512 (the MP = 512 kernel): the oracle's
+    assert np.all(p[s != 0] == 1.0)            # Jacobi solver takes ~1.5 s per window
 
 
 def test_general_path_literal_windows(oracle):
@@ -43,13 +44,14 @@ def test_general_path_literal_windows(oracle):
     _cmp(s, s_ref)
 
 
-@pytest.mark.parametrize("a,b,nsnp,treshold,runs", [(100, 100, 400, 10, 100), (70, 80, 500, 30, 150)])
+@pytest.mark.parametrize("a,b,nsnp,treshold,runs", [(100, 100, 400, 10, 100), (70, 80, 500, 30, 150),
+                                                  (150, 110, 120, 10, 40)])
 def test_general_path_permutations(oracle, a, b, nsnp, treshold, runs):
     from gdscan import css, synth
     av, bv, ap, bp, regend = synth.chromosome(220 + a, nsnp, a, b)
     s, p, X = css.scan_coords(av, bv, ap, bp, regend, treshold=treshold, runs=runs, seed=13, serial=True)
     s_ref, _ = oracle_css_scan(oracle, av, bv, ap, bp, regend, serial=True)
-    _cmp(s, s_ref)
+    _cmp(s, s_ref, 20 if nsnp > 200 else 6)
     bad = []
     for w in np.flatnonzero(s != 0):
         sc, p_lit, lo, hi, nt = _oracle_p(oracle, X[w], a, b, treshold, runs, 13, int(w))
