@@ -304,6 +304,7 @@ __device__ __forceinline__ double css_score(const int *tracks, int a, int b, Dis
  * steps): no division on the serial chain.  d (s_d) and e^2 (s_e2, e_{k-1}^2 at k,
  * s_e2[0] = 0) are padded to a multiple of 4 with decoupled entries above the
  * spectrum. */
+template <bool PREFETCH = false>
 __device__ __forceinline__ void bisect_top2(int m, double glo, double ghi, double bis_tol, const double *s_d,
                                             const double *s_e2, double *s_lam, int lane) {
   const int m4 = (m + 3) & ~3;
@@ -320,11 +321,26 @@ __device__ __forceinline__ void bisect_top2(int m, double glo, double ghi, doubl
      * spectrum, so the unrolled groups need no tail */
     double pm = 1.0, pc = 1.0;
     int cnt = 0;
+    double2 d01 = *reinterpret_cast<const double2 *>(s_d);
+    double2 d23 = *reinterpret_cast<const double2 *>(s_d + 2);
+    double2 e01 = *reinterpret_cast<const double2 *>(s_e2);
+    double2 e23 = *reinterpret_cast<const double2 *>(s_e2 + 2);
     for (int k = 0; k < m4; k += 4) {
-      const double2 d01 = *reinterpret_cast<const double2 *>(s_d + k);
-      const double2 d23 = *reinterpret_cast<const double2 *>(s_d + k + 2);
-      const double2 e01 = *reinterpret_cast<const double2 *>(s_e2 + k);
-      const double2 e23 = *reinterpret_cast<const double2 *>(s_e2 + k + 2);
+      if constexpr (!PREFETCH) {
+        d01 = *reinterpret_cast<const double2 *>(s_d + k);
+        d23 = *reinterpret_cast<const double2 *>(s_d + k + 2);
+        e01 = *reinterpret_cast<const double2 *>(s_e2 + k);
+        e23 = *reinterpret_cast<const double2 *>(s_e2 + k + 2);
+      }
+      /* PREFETCH (k_css_mds_t80): the next group's operands are loaded first */
+      double2 nd01 = d01, nd23 = d23, ne01 = e01, ne23 = e23;
+      if constexpr (PREFETCH) {
+        const int kn = k + 4 < m4 ? k + 4 : k;
+        nd01 = *reinterpret_cast<const double2 *>(s_d + kn);
+        nd23 = *reinterpret_cast<const double2 *>(s_d + kn + 2);
+        ne01 = *reinterpret_cast<const double2 *>(s_e2 + kn);
+        ne23 = *reinterpret_cast<const double2 *>(s_e2 + kn + 2);
+      }
       const double dk[4] = {d01.x, d01.y, d23.x, d23.y};
       const double ek[4] = {e01.x, e01.y, e23.x, e23.y}; /* e_{k-1}^2, s_e2[0] = 0 */
 #pragma unroll
@@ -339,6 +355,10 @@ __device__ __forceinline__ void bisect_top2(int m, double glo, double ghi, doubl
       const int ex = __builtin_amdgcn_frexp_exp(fmax(fabs(pm), fabs(pc)));
       pm = __builtin_amdgcn_ldexp(pm, -ex);
       pc = __builtin_amdgcn_ldexp(pc, -ex);
+      d01 = nd01;
+      d23 = nd23;
+      e01 = ne01;
+      e23 = ne23;
     }
     double nl = cnt <= target ? x : l;
     double nu = cnt <= target ? u : x;
@@ -373,19 +393,35 @@ __device__ __forceinline__ void invit_factor(int m, int e, const double *s_d, co
   double *ml = s_x + e * MP; /* elimination multipliers; s_x is free until X is formed */
   uint8_t *pv = s_piv[e];
   double cc0 = s_d[0] - sig, cc1 = m > 1 ? s_e[0] : 0.0;
-  for (int k = 0; k < m - 1; ++k) {
-    const double n0 = s_e[k], n1 = s_d[k + 1] - sig, n2 = (k + 2 < m) ? s_e[k + 1] : 0.0;
-    const bool sw = fabs(cc0) < fabs(n0);
-    const double pvt = sw ? n0 : cc0, oth = sw ? cc0 : n0;
-    const double t = (pvt != 0.0) ? oth * fast_rcp(pvt) : 0.0;
-    U0[k] = pvt;
-    U1[k] = sw ? n1 : cc1;
-    U2[k] = sw ? n2 : 0.0;
-    ml[k] = t;
-    pv[k] = sw;
-    const double nc0 = sw ? fma(-t, n1, cc1) : fma(-t, cc1, n1);
-    cc1 = sw ? -t * n2 : n2;
-    cc0 = nc0;
+  /* four steps' operands are loaded together: the stores of a block cannot be crossed
+   * by the compiler, so a load per step would wait out its LDS latency on the chain */
+  for (int k0 = 0; k0 < m - 1; k0 += 4) {
+    double n0v[4], n1v[4], n2v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int k = min(k0 + u, MP - 2);
+      n0v[u] = s_e[k];
+      n1v[u] = s_d[k + 1] - sig;
+      n2v[u] = (k0 + u + 2 < m) ? s_e[k + 1] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int k = k0 + u;
+      if (k < m - 1) {
+        const double n0 = n0v[u], n1 = n1v[u], n2 = n2v[u];
+        const bool sw = fabs(cc0) < fabs(n0);
+        const double pvt = sw ? n0 : cc0, oth = sw ? cc0 : n0;
+        const double t = (pvt != 0.0) ? oth * fast_rcp(pvt) : 0.0;
+        U0[k] = pvt;
+        U1[k] = sw ? n1 : cc1;
+        U2[k] = sw ? n2 : 0.0;
+        ml[k] = t;
+        pv[k] = sw;
+        const double nc0 = sw ? fma(-t, n1, cc1) : fma(-t, cc1, n1);
+        cc1 = sw ? -t * n2 : n2;
+        cc0 = nc0;
+      }
+    }
   }
   U0[m - 1] = cc0;
   /* start vector: deterministic, not orthogonal to anything in practice */
@@ -404,23 +440,55 @@ __device__ __forceinline__ void invit_solve(int m, int e, double (*s_lu)[3][MP],
   const double *R0 = s_lu[e][0], *U1 = s_lu[e][1], *U2 = s_lu[e][2], *ml = s_x + e * MP;
   const uint8_t *pv = s_piv[e];
   double yk = y[0];
-  for (int k = 0; k < m - 1; ++k) {
-    double yn = y[k + 1];
-    if (pv[k]) {
-      const double t = yk;
-      yk = yn;
-      yn = t;
+  /* operands four steps at a time (invit_factor); y[k + 1] is read before any store
+   * reaches it */
+  for (int k0 = 0; k0 < m - 1; k0 += 4) {
+    double ynv[4], mlv[4];
+    int pvv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int k = min(k0 + u, MP - 2);
+      ynv[u] = y[k + 1];
+      mlv[u] = ml[k];
+      pvv[u] = pv[k];
     }
-    y[k] = yk;
-    yk = fma(-ml[k], yk, yn);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int k = k0 + u;
+      if (k < m - 1) {
+        double yn = ynv[u];
+        if (pvv[u]) {
+          const double t = yk;
+          yk = yn;
+          yn = t;
+        }
+        y[k] = yk;
+        yk = fma(-mlv[u], yk, yn);
+      }
+    }
   }
   double z1 = yk * R0[m - 1], z2 = 0.0;
   y[m - 1] = z1;
-  for (int k = m - 2; k >= 0; --k) {
-    const double z0 = (y[k] - U1[k] * z1 - U2[k] * z2) * R0[k];
-    y[k] = z0;
-    z2 = z1;
-    z1 = z0;
+  for (int k0 = m - 2; k0 >= 0; k0 -= 4) {
+    double yv[4], u1v[4], u2v[4], r0v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int k = max(k0 - u, 0);
+      yv[u] = y[k];
+      u1v[u] = U1[k];
+      u2v[u] = U2[k];
+      r0v[u] = R0[k];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int k = k0 - u;
+      if (k >= 0) {
+        const double z0 = (yv[u] - u1v[u] * z1 - u2v[u] * z2) * r0v[u];
+        y[k] = z0;
+        z2 = z1;
+        z1 = z0;
+      }
+    }
   }
 }
 
@@ -1213,180 +1281,205 @@ __device__ __forceinline__ double quad_sum(double x) {
   return x + dpp64<0x4E, 0xF>(x, 0.0); /* quad_perm [2,3,0,1] */
 }
 
-/* Row K, v and w reach the main rows as LDS broadcasts (every lane reads the same
- * doubles: 64 x 8 B of LDS return bandwidth per double), or, with these switches, by
- * v_readlane from the lane that holds them (two VALU per double, SGPR operands). */
-#ifndef T80_RL_ROW
-#define T80_RL_ROW 0
-#endif
-#ifndef T80_RL_VW
-#define T80_RL_VW 0
-#endif
+/* Householder steps: one LDS round trip per step (the unfused form, hh_step_static,
+ * took two and ran C4 at 5.9 M windows/s against 7.2 M).  Row K of the
+ * matrix is read as column K (every lane holds its own entry, symmetric up to rounding),
+ * so the reflector's vector needs no single-lane publish: after step K's scalars every lane
+ * computes its entry of column K + 1 as it will be after the update (v_{K+1} = 1,
+ * w_{K+1} by v_readlane) and publishes it with v_i, w_i; one pass over the row then applies
+ * the rank-2 update and accumulates the next step's p = A r, four chains deep.  r and p
+ * travel to the next step in registers (T80Carry). */
+struct T80Carry {
+  double r, p, rt, pt; /* column K entry and p_i of this lane's main row and tail row */
+};
+
+/* the rank-2 update of this lane's rows over columns > K and p = A r over columns > K + 1
+ * (s_r holds 0 at rows <= K + 1) */
 template <int K>
-__device__ __forceinline__ double t80_row(const double (&A)[T80], const double *s_row, int j) {
-#if T80_RL_ROW
-  if constexpr (K < T80_MAIN) return readlane_f64(A[j], K);
+__device__ __forceinline__ void t80_fused_pass(double (&A)[T80], double vi, double wi, double vt, double wt,
+                                               const double2 *s_vw, const double *s_r,
+                                               double (*s_tail)[T80_TSTRIDE], T80Carry &c) {
+  constexpr int MP = T80;
+  const int i = css_lane_now(), tr = i >> 2, tq = i & 3;
+  double p[4] = {0.0, 0.0, 0.0, 0.0};
+#ifndef T80_FB
+#define T80_FB 4
 #endif
-  return s_row[j];
+  constexpr int FB = T80_FB; /* columns per pinned group (register pressure) */
+#pragma unroll
+  for (int jb = 0; jb < MP / FB; ++jb) {
+    if (FB * jb + FB - 1 > K) {
+#pragma unroll
+      for (int u = 0; u < FB; ++u) {
+        const int j = FB * jb + u;
+        if (j > K) {
+          const double2 vw = s_vw[j];
+          A[j] = fma(-vi, vw.y, fma(-wi, vw.x, A[j]));
+        }
+      }
+      /* pinned before the products read them: one live copy of each updated entry */
+#pragma unroll
+      for (int u = 0; u < FB; ++u) CSS_PIN(A[FB * jb + u]);
+#pragma unroll
+      for (int u = 0; u < FB; ++u) {
+        const int j = FB * jb + u;
+        if (j > K + 1) p[u & 3] = fma(A[j], s_r[j], p[u & 3]);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) CSS_PIN(p[u]);
+    }
+  }
+  A[K] = vi; /* stash v_K in the dead column K */
+  double *tw = s_tail[tr];
+  double t0 = 0.0, t1 = 0.0;
+#pragma unroll
+  for (int s = 0; s < T80_TS; ++s) {
+    if (4 * s + 3 > K) {
+      const int j = 4 * s + tq;
+      const double2 vw = s_vw[j]; /* v_j = w_j = 0 at j <= K: the dead columns stay */
+      const double t = fma(-vt, vw.y, fma(-wt, vw.x, tw[j]));
+      tw[j] = t;
+      if (s & 1)
+        t1 = fma(t, s_r[j], t1);
+      else
+        t0 = fma(t, s_r[j], t0);
+    }
+    if ((s & 3) == 3) {
+      CSS_PIN(t0);
+      CSS_PIN(t1);
+    }
+  }
+  if (tq == (K & 3)) tw[K] = vt;
+  c.p = (p[0] + p[1]) + (p[2] + p[3]);
+  c.pt = quad_sum(t0 + t1);
 }
 
-/* One Householder step (hh_step_static) over the main rows and the LDS tail. */
-template <int K>
-__device__ __forceinline__ void t80_step(double (&A)[T80], int m, double *s_row, double *s_v, double *s_w,
-                                         double *s_d, double *s_e, double *s_tau, double (*s_tail)[T80_TSTRIDE]) {
+/* column 0 and p = A r before step 0 */
+__device__ __forceinline__ void t80_fused_start(const double (&A)[T80], int m, double2 *s_vw, double *s_r, double *s_d,
+                                                double (*s_tail)[T80_TSTRIDE], T80Carry &c) {
   constexpr int MP = T80;
   const int i = css_lane_now(), tr = i >> 2, tq = i & 3, R = T80_MAIN + tr;
+  (void)m;
+  c.r = A[0];
+  c.rt = s_tail[tr][0];
+  __syncthreads();
+  s_r[i] = i > 0 ? c.r : 0.0;
+  if (tq == 0) s_r[R] = c.rt;
+  if (i == 0) s_d[0] = c.r;
+  __syncthreads();
+  double p[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int j = 1; j < MP; ++j) {
+    p[j & 3] = fma(A[j], s_r[j], p[j & 3]);
+    if ((j & 7) == 7) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) CSS_PIN(p[u]);
+    }
+  }
+  const double *trw = s_tail[tr];
+  double t0 = 0.0, t1 = 0.0;
+#pragma unroll
+  for (int s = 0; s < T80_TS; ++s) {
+    const int j = 4 * s + tq;
+    if (s & 1)
+      t1 = fma(trw[j], s_r[j], t1);
+    else
+      t0 = fma(trw[j], s_r[j], t0);
+  }
+  c.p = (p[0] + p[1]) + (p[2] + p[3]);
+  c.pt = quad_sum(t0 + t1);
+  (void)s_vw;
+}
+
+/* One fused Householder step K <= MP - 3 (hh_step_static's arithmetic) */
+template <int K>
+__device__ __forceinline__ void t80_fstep(double (&A)[T80], int m, T80Carry &c, double2 *s_vw, double *s_r,
+                                          double *s_d, double *s_e, double *s_tau, double (*s_tail)[T80_TSTRIDE]) {
+  const int i = css_lane_now(), tr = i >> 2, tq = i & 3, R = T80_MAIN + tr;
   const bool row = i < m, trow = R < m;
-  __syncthreads();
-  if constexpr (K < T80_MAIN) {
-    if (i == K) {
-#pragma unroll
-      for (int jb = 0; jb < MP / 8; ++jb)
-        if (8 * jb + 7 >= K) {
-#pragma unroll
-          for (int u = 0; u < 8; u += 2) {
-            const int j = 8 * jb + u;
-            *reinterpret_cast<double2 *>(s_row + j) = make_double2(j > K ? A[j] : 0.0, j + 1 > K ? A[j + 1] : 0.0);
-          }
-        }
-      s_d[K] = A[K];
-    }
+  const double xi = (i > K + 1 && row) ? c.r : 0.0;
+  const double xr = (R > K + 1 && trow) ? c.rt : 0.0;
+  /* |x|^2 and r^T A r in one reduction; a tail row counts once */
+  double sigma = xi * xi + (tq == 0 ? xr * xr : 0.0);
+  double q = ((i > K && row) ? c.r * c.p : 0.0) + ((tq == 0 && R > K && trow) ? c.rt * c.pt : 0.0);
+  wave_sum2(sigma, q);
+  double alpha, pr1, a11;
+  if constexpr (K + 1 < T80_MAIN) {
+    alpha = readlane_f64(c.r, K + 1);
+    pr1 = readlane_f64(c.p, K + 1);
+    a11 = readlane_f64(A[K + 1], K + 1);
   } else {
-    const double *src = s_tail[K - T80_MAIN];
-    s_row[i] = i > K ? src[i] : 0.0;
-    if (i + 64 < MP) s_row[i + 64] = i + 64 > K ? src[i + 64] : 0.0;
-    if (i == 0) s_d[K] = src[K];
+    alpha = readlane_f64(c.rt, 4 * (K + 1 - T80_MAIN));
+    pr1 = readlane_f64(c.pt, 4 * (K + 1 - T80_MAIN));
+    a11 = s_tail[K + 1 - T80_MAIN][K + 1];
+  }
+  double tau = 0.0, beta = alpha, scale = 0.0;
+  if (sigma != 0.0) {
+    beta = -copysign(sqrt(alpha * alpha + sigma), alpha);
+    const double rr = fast_rcp(beta * (alpha - beta));
+    tau = -(alpha - beta) * (alpha - beta) * rr;
+    scale = beta * rr;
+  }
+  const double Kc = -0.5 * tau * (tau * scale * scale) * fma(beta, fma(beta, a11, -2.0 * pr1), q);
+  const double ak1 = A[K + 1];
+  const double vi = (i == K + 1) ? 1.0 : xi * scale;
+  const double pi = (i > K && row) ? (tau * scale) * fma(-beta, ak1, c.p) : 0.0;
+  const double wi = fma(Kc, vi, pi);
+  const double akt = s_tail[tr][K + 1];
+  const double vt = (R == K + 1) ? 1.0 : xr * scale;
+  const double ptl = (R > K && trow) ? (tau * scale) * fma(-beta, akt, c.pt) : 0.0;
+  const double wt = fma(Kc, vt, ptl);
+  double wk1;
+  if constexpr (K + 1 < T80_MAIN)
+    wk1 = readlane_f64(wi, K + 1);
+  else
+    wk1 = readlane_f64(wt, 4 * (K + 1 - T80_MAIN));
+  /* column K + 1 after this step (the update's formula at v_{K+1} = 1) */
+  const double rn = fma(-vi, wk1, fma(-wi, 1.0, ak1));
+  const double rnt = fma(-vt, wk1, fma(-wt, 1.0, akt));
+  __syncthreads();
+  if (i == 0) {
+    s_e[K] = beta;
+    s_tau[K] = tau;
+  }
+  s_vw[i] = make_double2(vi, wi);
+  s_r[i] = i > K + 1 ? rn : 0.0;
+  if (tq == 0) {
+    s_vw[R] = make_double2(vt, wt);
+    s_r[R] = R > K + 1 ? rnt : 0.0;
+  }
+  if constexpr (K + 1 < T80_MAIN) {
+    if (i == K + 1) s_d[K + 1] = rn;
+  } else {
+    if (i == 4 * (K + 1 - T80_MAIN)) s_d[K + 1] = rnt;
   }
   __syncthreads();
-  if constexpr (K >= MP - 2) {
-    if (i == 0 && K == m - 2) s_e[K] = s_row[K + 1];
-    return;
-  } else {
-    /* K >= m - 2 below MP - 2: a no-op reflector on the zero padding (hh_step_static) */
-    const double xi = (i > K + 1 && row) ? s_row[i] : 0.0;
-    const double alpha = s_row[K + 1];
-    double p0 = 0, p1 = 0;
-#pragma unroll
-    for (int jb = 0; jb < MP / 8; ++jb) {
-      if (8 * jb + 7 > K) {
-#pragma unroll
-        for (int u = 0; u < 8; u += 2) {
-          if (8 * jb + u > K) p0 = fma(A[8 * jb + u], t80_row<K>(A, s_row, 8 * jb + u), p0);
-          if (8 * jb + u + 1 > K) p1 = fma(A[8 * jb + u + 1], t80_row<K>(A, s_row, 8 * jb + u + 1), p1);
-        }
-        CSS_PIN(p0);
-        CSS_PIN(p1);
-      }
-    }
-    const double ak1 = A[K + 1];
-    const double praw = p0 + p1;
-    /* the tail row over the live column groups (4s + 3 > K; s_row is 0 at j <= K) */
-    const double *trw = s_tail[tr];
-    double t0 = 0, t1 = 0;
-#pragma unroll
-    for (int s = 0; s < T80_TS; ++s) {
-      if (4 * s + 3 > K) {
-        const int j = 4 * s + tq;
-        if (s & 1)
-          t1 = fma(trw[j], s_row[j], t1);
-        else
-          t0 = fma(trw[j], s_row[j], t0);
-      }
-      if ((s & 3) == 3) {
-        CSS_PIN(t0);
-        CSS_PIN(t1);
-      }
-    }
-    const double pt = quad_sum(t0 + t1);
-    const double akt = trw[K + 1];
-    const double xr = (R > K + 1 && trow) ? s_row[R] : 0.0;
-    /* |x|^2 and r^T A r in one reduction (hh_step_static); a tail row counts once */
-    double sigma = xi * xi + (tq == 0 ? xr * xr : 0.0);
-    double q = ((i > K && row) ? s_row[i] : 0.0) * praw + ((tq == 0 && R > K && trow) ? s_row[R] * pt : 0.0);
-    wave_sum2(sigma, q);
-    double pr1, a11;
-    if constexpr (K + 1 < T80_MAIN) {
-      pr1 = readlane_f64(praw, K + 1);
-      a11 = readlane_f64(ak1, K + 1);
-    } else {
-      pr1 = readlane_f64(pt, 4 * (K + 1 - T80_MAIN));
-      a11 = readlane_f64(akt, 4 * (K + 1 - T80_MAIN));
-    }
-    double tau = 0.0, beta = alpha, scale = 0.0;
-    if (sigma != 0.0) {
-      beta = -copysign(sqrt(alpha * alpha + sigma), alpha);
-      const double r = fast_rcp(beta * (alpha - beta));
-      tau = -(alpha - beta) * (alpha - beta) * r;
-      scale = beta * r;
-    }
-    const double Kc = -0.5 * tau * (tau * scale * scale) * fma(beta, fma(beta, a11, -2.0 * pr1), q);
-    const double vi = (i == K + 1) ? 1.0 : xi * scale;
-    const double pi = (i > K && row) ? (tau * scale) * fma(-beta, ak1, praw) : 0.0;
-    const double wi = fma(Kc, vi, pi);
-    const double vt = (R == K + 1) ? 1.0 : xr * scale;
-    const double ptl = (R > K && trow) ? (tau * scale) * fma(-beta, akt, pt) : 0.0;
-    const double wt = fma(Kc, vt, ptl);
-    if (i == 0) {
-      s_e[K] = beta;
-      s_tau[K] = tau;
-    }
-    s_v[i] = vi;
-    s_w[i] = wi;
-    if (tq == 0) {
-      s_v[R] = vt;
-      s_w[R] = wt;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int jb = 0; jb < MP / 8; ++jb) {
-      if (8 * jb + 7 > K) {
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          const int j = 8 * jb + u;
-          if (j > K) {
-#if T80_RL_VW
-            /* v_j, w_j from the lane that computed them (row j < 64: lane j; tail row j:
-             * lane 4 (j - 64)) as SGPR operands instead of LDS broadcasts */
-            const int src = j < T80_MAIN ? j : 4 * (j - T80_MAIN);
-            const double wj = readlane_f64(j < T80_MAIN ? wi : wt, src);
-            const double vj = readlane_f64(j < T80_MAIN ? vi : vt, src);
-#else
-            const double wj = s_w[j], vj = s_v[j];
-#endif
-            A[j] = fma(-vi, wj, fma(-wi, vj, A[j]));
-          }
-        }
-#pragma unroll
-        for (int u = 0; u < 8; ++u) CSS_PIN(A[8 * jb + u]);
-      }
-    }
-    A[K] = vi; /* stash v_K in the dead column K */
-    double *tw = s_tail[tr];
-#pragma unroll
-    for (int s = 0; s < T80_TS; ++s) {
-      if (4 * s + 3 > K) {
-        const int j = 4 * s + tq;
-        tw[j] = fma(-vt, s_w[j], fma(-wt, s_v[j], tw[j]));
-      }
-    }
-    if (tq == (K & 3)) tw[K] = vt;
-  }
+  t80_fused_pass<K>(A, vi, wi, vt, wt, s_vw, s_r, s_tail, c);
+  c.r = rn;
+  c.rt = rnt;
 }
 
 template <int K>
-struct T80Steps {
-  static __device__ __forceinline__ void run(double (&A)[T80], int m, double *s_row, double *s_v, double *s_w,
+struct T80FSteps {
+  static __device__ __forceinline__ void run(double (&A)[T80], int m, T80Carry &c, double2 *s_vw, double *s_r,
                                              double *s_d, double *s_e, double *s_tau, double (*s_tail)[T80_TSTRIDE]) {
     if ((K & 7) == 0 && K >= m) return; /* exits only at block boundaries (hh_step_static) */
-    t80_step<K>(A, m, s_row, s_v, s_w, s_d, s_e, s_tau, s_tail);
-    T80Steps<K + 1>::run(A, m, s_row, s_v, s_w, s_d, s_e, s_tau, s_tail);
+    if constexpr (K <= T80 - 3) {
+      t80_fstep<K>(A, m, c, s_vw, s_r, s_d, s_e, s_tau, s_tail);
+      T80FSteps<K + 1>::run(A, m, c, s_vw, s_r, s_d, s_e, s_tau, s_tail);
+    } else {
+      /* K = MP - 2: no reflector; e_{MP-2} = column MP - 2 at row MP - 1, d_{MP-1} */
+      const int i = css_lane_now();
+      const double e = readlane_f64(c.rt, 4 * (T80 - 1 - T80_MAIN));
+      __syncthreads();
+      if (i == 0) {
+        if (K == m - 2) s_e[K] = e;
+        s_d[K + 1] = s_tail[T80 - 1 - T80_MAIN][T80 - 1];
+      }
+    }
   }
 };
-template <>
-struct T80Steps<T80> {
-  static __device__ __forceinline__ void run(double (&)[T80], int, double *, double *, double *, double *, double *,
-                                             double *, double (*)[T80_TSTRIDE]) {}
-};
+
 }  // namespace
 
 __global__ void __launch_bounds__(64, 2)
@@ -1400,8 +1493,8 @@ __global__ void __launch_bounds__(64, 2)
   __shared__ __attribute__((aligned(16))) union {
     struct {
       double e2[MP + 4]; /* bisection only (after the Householder steps) */
-      double row[MP + 2];
-      double v[MP], w[MP];
+      double r[MP + 2]; /* Householder steps: column K + 1; row means before them */
+      double2 vw[MP];   /* Householder steps: (v_j, w_j), 16-B aligned */
       uint64_t mask[2 * MP];
       double vals[MP];
     } a;
@@ -1616,11 +1709,11 @@ __global__ void __launch_bounds__(64, 2)
       rst = quad_sum(rst);
       const double ri = row ? rs / m : 0.0, rt = trow ? rst / m : 0.0;
       __syncthreads();
-      s_u.a.v[i] = ri;
-      if (tq == 0) s_u.a.v[R] = rt;
+      s_u.a.r[i] = ri;
+      if (tq == 0) s_u.a.r[R] = rt;
       const double g = block_sum<1>(ri + (tq == 0 ? rt : 0.0), s_red) / m;
       __syncthreads();
-      const double *sv = s_u.a.v;
+      const double *sv = s_u.a.r;
       CSS_OPAQUE_S(mo);
 #pragma unroll
       for (int jj = 0; jj < MP; ++jj) {
@@ -1648,7 +1741,11 @@ __global__ void __launch_bounds__(64, 2)
     CSS_PROF(1);
     /* ---- Householder tridiagonalisation (LAPACK dsytd2, lower; k_css_mds) */
 #ifndef GD_CSS_SKIP_TRIDIAG
-    T80Steps<0>::run(A, m, s_u.a.row, s_u.a.v, s_u.a.w, s_d, s_e, s_tau, s_tail);
+    {
+      T80Carry cr;
+      t80_fused_start(A, m, s_u.a.vw, s_u.a.r, s_d, s_tail, cr);
+      T80FSteps<0>::run(A, m, cr, s_u.a.vw, s_u.a.r, s_d, s_e, s_tau, s_tail);
+    }
 #endif
     __syncthreads();
 
@@ -1678,7 +1775,7 @@ __global__ void __launch_bounds__(64, 2)
     }
     const double bis_tol = CSS_BISECT_TOL * fmax(fabs(glo), fabs(ghi)) + DBL_MIN;
     __syncthreads();
-    bisect_top2(m, glo, ghi, bis_tol, s_d, s_e2, s_lam, tid);
+    bisect_top2<true>(m, glo, ghi, bis_tol, s_d, s_e2, s_lam, tid);
     __syncthreads();
 
     CSS_PROF(3);
