@@ -1306,47 +1306,97 @@ __device__ __forceinline__ void t80_fused_pass(double (&A)[T80], double vi, doub
 #define T80_FB 4
 #endif
   constexpr int FB = T80_FB; /* columns per pinned group (register pressure) */
+  /* software-pipelined: group jb + 1's (v, w) and r are loaded before group jb is
+   * computed, so a group waits on loads issued one group earlier; the pins' memory
+   * clobbers keep the loads of later groups below them (bounded registers) */
+  constexpr int NB = MP / FB, JB0 = (K + 1) / FB;
+  double2 cvw[FB];
+  double cr[FB];
 #pragma unroll
-  for (int jb = 0; jb < MP / FB; ++jb) {
-    if (FB * jb + FB - 1 > K) {
+  for (int u = 0; u < FB; ++u) {
+    cvw[u] = s_vw[FB * JB0 + u];
+    cr[u] = s_r[FB * JB0 + u];
+  }
+#pragma unroll
+  for (int jb = JB0; jb < NB; ++jb) {
+    double2 nvw[FB];
+    double nr[FB];
+    if (jb + 1 < NB) {
 #pragma unroll
       for (int u = 0; u < FB; ++u) {
-        const int j = FB * jb + u;
-        if (j > K) {
-          const double2 vw = s_vw[j];
-          A[j] = fma(-vi, vw.y, fma(-wi, vw.x, A[j]));
-        }
+        nvw[u] = s_vw[FB * (jb + 1) + u];
+        nr[u] = s_r[FB * (jb + 1) + u];
       }
-      /* pinned before the products read them: one live copy of each updated entry */
+    }
 #pragma unroll
-      for (int u = 0; u < FB; ++u) CSS_PIN(A[FB * jb + u]);
+    for (int u = 0; u < FB; ++u) {
+      const int j = FB * jb + u;
+      if (j > K) A[j] = fma(-vi, cvw[u].y, fma(-wi, cvw[u].x, A[j]));
+    }
+#pragma unroll
+    for (int u = 0; u < FB; ++u) CSS_PIN(A[FB * jb + u]);
+#pragma unroll
+    for (int u = 0; u < FB; ++u) {
+      const int j = FB * jb + u;
+      if (j > K + 1) p[u & 3] = fma(A[j], cr[u], p[u & 3]);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) CSS_PIN(p[u]);
+    if (jb + 1 < NB) {
 #pragma unroll
       for (int u = 0; u < FB; ++u) {
-        const int j = FB * jb + u;
-        if (j > K + 1) p[u & 3] = fma(A[j], s_r[j], p[u & 3]);
+        cvw[u] = nvw[u];
+        cr[u] = nr[u];
       }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) CSS_PIN(p[u]);
     }
   }
   A[K] = vi; /* stash v_K in the dead column K */
   double *tw = s_tail[tr];
   double t0 = 0.0, t1 = 0.0;
+  constexpr int TG = 2, S0 = (K + 1) / 4 / TG * TG; /* tail groups of TG column quads */
+  double ct[TG], ctr[TG];
+  double2 ctv[TG];
 #pragma unroll
-  for (int s = 0; s < T80_TS; ++s) {
-    if (4 * s + 3 > K) {
-      const int j = 4 * s + tq;
-      const double2 vw = s_vw[j]; /* v_j = w_j = 0 at j <= K: the dead columns stay */
-      const double t = fma(-vt, vw.y, fma(-wt, vw.x, tw[j]));
-      tw[j] = t;
-      if (s & 1)
-        t1 = fma(t, s_r[j], t1);
-      else
-        t0 = fma(t, s_r[j], t0);
+  for (int u = 0; u < TG; ++u) {
+    const int j = 4 * (S0 + u) + tq;
+    ct[u] = tw[j];
+    ctv[u] = s_vw[j];
+    ctr[u] = s_r[j];
+  }
+#pragma unroll
+  for (int sg = S0; sg < T80_TS; sg += TG) {
+    double nt[TG], ntr[TG];
+    double2 ntv[TG];
+    if (sg + TG < T80_TS) {
+#pragma unroll
+      for (int u = 0; u < TG; ++u) {
+        const int j = 4 * (sg + TG + u) + tq;
+        nt[u] = tw[j];
+        ntv[u] = s_vw[j];
+        ntr[u] = s_r[j];
+      }
     }
-    if ((s & 3) == 3) {
-      CSS_PIN(t0);
-      CSS_PIN(t1);
+#pragma unroll
+    for (int u = 0; u < TG; ++u) {
+      const int j = 4 * (sg + u) + tq;
+      if (4 * (sg + u) + 3 > K) { /* v_j = w_j = 0 at j <= K: the dead columns stay */
+        const double t = fma(-vt, ctv[u].y, fma(-wt, ctv[u].x, ct[u]));
+        tw[j] = t;
+        if (u & 1)
+          t1 = fma(t, ctr[u], t1);
+        else
+          t0 = fma(t, ctr[u], t0);
+      }
+    }
+    CSS_PIN(t0);
+    CSS_PIN(t1);
+    if (sg + TG < T80_TS) {
+#pragma unroll
+      for (int u = 0; u < TG; ++u) {
+        ct[u] = nt[u];
+        ctv[u] = ntv[u];
+        ctr[u] = ntr[u];
+      }
     }
   }
   if (tq == (K & 3)) tw[K] = vt;
