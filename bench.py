@@ -424,6 +424,8 @@ class Env:
         self.args, self.rank, self.world, self.dist = args, rank, world, dist
         self.torch, self._lib, self.synth, self.Chrom, self.check, self.lib = torch, _lib, synth, Chrom, check, lib
         self.dev = torch.device("cuda", local)
+        # gloo (ranks sharing a GPU, or --backend gloo) reduces host tensors; RCCL device ones
+        self.cdev = torch.device("cpu") if dist and dist.get_backend() == "gloo" else self.dev
         self.stream = torch.cuda.current_stream(self.dev).cuda_stream
         self.ctx = lib.gd_ctx_create(local)
         assert self.ctx, "gd_ctx_create failed"
@@ -431,7 +433,7 @@ class Env:
     def max_over_ranks(self, x):
         if not self.dist:
             return x
-        t = self.torch.tensor([x], dtype=self.torch.float64, device=self.dev)
+        t = self.torch.tensor([x], dtype=self.torch.float64, device=self.cdev)
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
         return float(t.item())
 
@@ -628,7 +630,7 @@ def c45_leg(env, args, name, treshold, runs, queue):
             local = torch.stack([sc[:nout], pv[:nout]], 1)
         env.sync()
         g0 = time.perf_counter()
-        track = gather_tracks(local, shard_done, wins)
+        track = gather_tracks(local.to(env.cdev), shard_done, wins)
         torch.cuda.synchronize()
         out["track_gather_ms"] = env.max_over_ranks((time.perf_counter() - g0) * 1e3)
         sc_all, p_all = track[:, 0], track[:, 1]
@@ -659,7 +661,7 @@ def c45_leg(env, args, name, treshold, runs, queue):
     if runs > 0 and computed.any():
         perm_ms = float(stage[1])
         if env.dist:  # GPU-time of the permutation kernel summed over ranks
-            t = torch.tensor([perm_ms], dtype=torch.float64, device=env.dev)
+            t = torch.tensor([perm_ms], dtype=torch.float64, device=env.cdev)
             env.dist.all_reduce(t)
             perm_ms = float(t.item())
         out["permutations"] = perm_stats(pm, computed, treshold, runs, perm_ms, pop)
@@ -728,10 +730,21 @@ def main():
         else:
             print(json.dumps({"dry_run": True, "n_gpus": 1}), flush=True)
         return
+    # more ranks than GPUs (a rehearsal of --gpus N on a smaller box): ranks share the
+    # devices round-robin, and the collectives go over gloo (RCCL refuses two ranks on one
+    # GPU); device_count() does not initialise the GPU
+    ndev = max(1, torch.cuda.device_count())
+    shared = world > ndev
+    if shared and args.backend == "nccl":
+        args.backend = "gloo"
+    local = local % ndev
     torch.cuda.set_device(local)
     if world > 1:
         import torch.distributed as dist_mod
-        dist_mod.init_process_group(args.backend, device_id=torch.device("cuda", local))
+        if args.backend == "gloo":
+            dist_mod.init_process_group("gloo")
+        else:
+            dist_mod.init_process_group(args.backend, device_id=torch.device("cuda", local))
         dist = dist_mod
 
     env = Env(args, rank, world, local, dist)
@@ -791,14 +804,14 @@ def main():
         # the one collective of the path: all ranks' (score, stddev) tracks gathered in
         # genome order; measured once, outside the timed steps
         from gdscan.shard import gather_tracks
-        wt = torch.zeros(world * nch, dtype=torch.int64, device=dev)
+        wt = torch.zeros(world * nch, dtype=torch.int64, device=env.cdev)
         wt[rank * nch:(rank + 1) * nch] = torch.tensor([chroms[c].regend // args.wstep for c in range(nch)])
         dist.all_reduce(wt)  # every rank learns every chromosome's window count
         shards = [list(range(r * nch, (r + 1) * nch)) for r in range(world)]
         loc = torch.stack([scores, stddev], 1)
         env.sync()
         g0 = time.perf_counter()
-        gather_tracks(loc, shards, wt.tolist())
+        gather_tracks(loc.to(env.cdev), shards, wt.tolist())
         torch.cuda.synchronize()
         gather_ms = env.max_over_ranks((time.perf_counter() - g0) * 1e3)
     total_windows = windows * world
@@ -825,6 +838,7 @@ def main():
                         "wsize 2500, wstep 500, perc 0.95, 100 bootstrap replicates",
             "chromosomes_per_gpu": nch, "snps_per_gpu": nch * nsnp, "windows_per_gpu": windows,
             "asize": a, "bsize": b, "parallelism": f"window-sharded x{world} (whole chromosomes per rank)",
+            "ranks_per_gpu": -(-world // ndev), "collective_backend": args.backend if world > 1 else None,
             "track_gather_ms": gather_ms,
         },
         "roofline": {
