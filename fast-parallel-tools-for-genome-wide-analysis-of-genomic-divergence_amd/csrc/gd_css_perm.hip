@@ -76,6 +76,9 @@ __device__ __forceinline__ double perm_xdist(const double *X, int i, int j) {
   return sqrt(dx * dx + dy * dy);
 }
 
+#ifndef PERM_CHAINS
+#define PERM_CHAINS 1 /* composition chains per wave (1 or 2), see k_css_perm phase 2 */
+#endif
 #ifndef PERM_MFMA
 #define PERM_MFMA 1 /* the permutation score on the matrix cores up to 80 individuals */
 #endif
@@ -370,20 +373,6 @@ __device__ __forceinline__ void score_f32(const float *S32, const double *R, con
 typedef _Float16 pm_f16x8 __attribute__((ext_vector_type(8)));
 typedef float pm_f32x16 __attribute__((ext_vector_type(16)));
 
-/* index of the k-th set bit of (lo, hi), k < popcount */
-__device__ __forceinline__ uint32_t pm_kth_bit(uint64_t lo, uint64_t hi, int k) {
-  const int c = __popcll(lo);
-  uint64_t x = lo;
-  uint32_t base = 0;
-  if (k >= c) {
-    k -= c;
-    x = hi;
-    base = 64;
-  }
-  while (k-- > 0) x &= x - 1;
-  return base + (uint32_t)__builtin_ctzll(x);
-}
-
 /* The score of every lane's track on the matrix cores (the between-group sum of
  * css.c:608-647 as a bilinear form).  With x_p the indicator of group A under
  * permutation p, bet_p = sum_{i in A, j in B} S_ij = x_p^T S (1 - x_p): one wave forms
@@ -397,47 +386,60 @@ __device__ __forceinline__ uint32_t pm_kth_bit(uint64_t lo, uint64_t hi, int k) 
  * 0/1 are exact; each Y entry takes <= 16 KT fp32 roundings and each dot <= 32 MT + 1
  * more, so |bet - est| <= (2^-10 + u (16 KT + 32 MT + 4)) bet + a b 2^-25 / sc; the pair
  * sums likewise with their term counts.  est and err as score_f32: |score_exact - est|
- * <= err, and the few lanes inside the bound recompute in FP64.  Also returns the lane's
- * group-A membership (alo, ahi). */
+ * <= err, and the few lanes inside the bound recompute in FP64. */
 template <int MP>
 __device__ __forceinline__ void score_mfma(const char *s16, const uint2 *lut, const uint8_t *col, const uint8_t *fmap,
                                            bool mapped, int a, int b, double inva, double invb, double inv_sc,
-                                           int lane, double &est, double &err, uint64_t &alo, uint64_t &ahi) {
+                                           int lane, double &est, double &err) {
   using SH = PermShape<MP>;
   constexpr int MT = SH::MT, KT = SH::KT, RS = SH::RS;
+  static_assert(MP <= 96, "score_mfma keeps members 64.. in one 32-bit word");
   const int m = a + b;
-  auto track = [&](int k) -> uint32_t {
-    const uint32_t c = col[k * PERM_ROW];
-    return mapped ? (uint32_t)fmap[c] : c;
-  };
-  auto s_at = [&](uint32_t x, uint32_t y) -> float {
-    return (float)*reinterpret_cast<const _Float16 *>(s16 + x * RS + 2 * y);
-  };
-  /* group A's members and the consecutive pairs */
   uint64_t lo = 0, hi = 0;
-  auto add = [&](uint32_t x) {
-    lo |= x < 64 ? 1ull << (x & 63u) : 0ull;
-    if constexpr (MP > 64) hi |= x >= 64 ? 1ull << (x & 63u) : 0ull;
+  auto s_at = [&](uint32_t x, uint32_t y) -> float {
+    return (float)*reinterpret_cast<const _Float16 *>(s16 + __umul24(x, (uint32_t)RS) + 2 * y);
   };
+  uint32_t hi32 = 0; /* members 64 .. MP - 1 (MP <= 96) */
+  auto add = [&](uint32_t x) {
+    const uint64_t t = 1ull << (x & 63u);
+    if constexpr (MP > 64) {
+      const bool h = x >= 64u;
+      lo |= h ? 0ull : t;
+      hi32 |= h ? (uint32_t)t : 0u;
+    } else {
+      lo |= t;
+    }
+  };
+  /* group A's members and the consecutive pairs, 16 track entries at a time: the
+   * entries' loads, their map lookups and the pair gathers each go out as one batch
+   * (one wait per batch instead of a round trip per entry) */
   float wa = 0.f, wb = 0.f;
-  uint32_t prev = track(0);
-  if (a > 0) add(prev);
-#pragma unroll 4
-  for (int k = 1; k < a; ++k) {
-    const uint32_t cur = track(k);
-    wa += s_at(prev, cur);
-    add(cur);
-    prev = cur;
+  uint32_t prev = 0;
+  constexpr int CK = 16; /* rows m .. MP - 1 of the byte matrix hold 0 (sig_identity) */
+#pragma unroll
+  for (int k0 = 0; k0 < MP; k0 += CK) {
+    if (k0 < m) {
+      uint32_t c[CK];
+#pragma unroll
+      for (int i = 0; i < CK; ++i) c[i] = k0 + i < MP ? (uint32_t)col[(k0 + i) * PERM_ROW] : 0u;
+      if (mapped) {
+#pragma unroll
+        for (int i = 0; i < CK; ++i) c[i] = fmap[c[i]];
+      }
+      float e[CK];
+#pragma unroll
+      for (int i = 0; i < CK; ++i) e[i] = s_at(i == 0 ? prev : c[i - 1], c[i]);
+#pragma unroll
+      for (int i = 0; i < CK; ++i) {
+        const int k = k0 + i;
+        if (k >= 1 && k < a) wa += e[i];
+        if (k > a && k < m) wb += e[i];
+        if (k < a) add(c[i]);
+      }
+      prev = c[CK - 1];
+    }
   }
-  if (a < m) prev = track(a);
-#pragma unroll 4
-  for (int k = a + 1; k < m; ++k) {
-    const uint32_t cur = track(k);
-    wb += s_at(prev, cur);
-    prev = cur;
-  }
-  alo = lo;
-  ahi = hi;
+  hi = hi32;
   const uint64_t vlo = m >= 64 ? ~0ull : ((1ull << m) - 1), vhi = m > 64 ? ((1ull << (m - 64)) - 1) : 0ull;
   const uint64_t clo = ~lo & vlo, chi = ~hi & vhi; /* group B = the complement within m */
   /* the masks of the two permutations whose columns this lane's fragments carry */
@@ -516,11 +518,14 @@ __device__ __forceinline__ void score_mfma(const char *s16, const uint2 *lut, co
 }
 
 /* every lane's column of one wave's byte matrix := identity (rows k < m; row k is
- * 64 bytes of k) */
+ * 64 bytes of k), rows m .. MP - 1 := 0 (score_mfma reads whole 16-row batches) */
+template <int MP>
 __device__ __forceinline__ void sig_identity(uint8_t *sig, int m, int lane) {
   PERM_OPAQUE(lane);
-  for (int q = lane; q < m * 16; q += 64)
-    *reinterpret_cast<uint32_t *>(sig + (q >> 4) * PERM_ROW + (q & 15) * 4) = (uint32_t)(q >> 4) * 0x01010101u;
+  for (int q = lane; q < MP * 16; q += 64) {
+    const uint32_t k = (uint32_t)(q >> 4);
+    *reinterpret_cast<uint32_t *>(sig + (q >> 4) * PERM_ROW + (q & 15) * 4) = k < (uint32_t)m ? k * 0x01010101u : 0u;
+  }
 }
 
 /* random_int_nrand48(n) constants for 2 <= n <= 128 from the magic number alone
@@ -538,26 +543,96 @@ __device__ __forceinline__ gd_randint perm_rd(uint32_t n, uint32_t magic) {
   return d;
 }
 
+#ifndef PERM_FY_PIPE
+#define PERM_FY_PIPE 0 /* software-pipelined Fisher-Yates (reads one step ahead, forwarded): measured
+                        * slower (the draw phase is issue-bound; forwarding adds 4 VALU per step) */
+#endif
+
+/* the magic number of n from VGPR lanes (lane l holds mag[l] in vm0, mag[64 + l] in vm1;
+ * n wave-uniform): no LDS round trip in the draw chain */
+__device__ __forceinline__ uint32_t perm_mag(uint32_t vm0, uint32_t vm1, int n) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)vm0, n & 63);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)vm1, n & 63);
+  return n < 64 ? lo : hi;
+}
+
 /* Fisher-Yates swaps of random_shuffle (css.c:700-706) on the lane's column, draws
  * from state x (no rejection: the caller checks); returns true if a draw would have
- * been rejected.  The next step's magic is read one step ahead. */
-__device__ __forceinline__ bool fy_fast(uint8_t *col, uint64_t x, int m, const uint32_t *mag) {
+ * been rejected.
+ *
+ * Software-pipelined: step n swaps positions n - 1 and j_n.  The two reads of step
+ * n - 1 are issued before the two writes of step n (LDS is in order per wave, so they
+ * see every write up to step n + 1), and step n's writes are forwarded in registers:
+ * position n - 2 or j_{n-1} holds u_n iff it equals j_n (position n - 1, written with
+ * v_n, is never read again).  Each step then waits for reads issued one step earlier
+ * instead of a full read -> write round trip.  The loop body is two steps with their
+ * own registers (A, B), so no loaded value is copied across the back edge (a copy
+ * would wait for the load). */
+__device__ __forceinline__ bool fy_fast(uint8_t *col, uint64_t x, int m, uint32_t vm0, uint32_t vm1) {
   bool rej = false;
-  uint32_t mg = __builtin_amdgcn_readfirstlane(mag[m]);
   /* the LCG on y = x << 16 (mod 2^64): no 48-bit mask, the draw is y >> 33 */
   uint64_t y = x << 16;
-  for (int s = 0; s < m - 1; ++s) {
-    const int n = __builtin_amdgcn_readfirstlane(m - s); /* wave-uniform */
-    const gd_randint rd = perm_rd((uint32_t)n, mg);
-    mg = __builtin_amdgcn_readfirstlane(mag[n - 1]);
+  auto draw = [&](int n) -> uint32_t { /* j_n = r mod n (n >= 2, wave-uniform) */
+    const gd_randint rd = perm_rd((uint32_t)n, perm_mag(vm0, vm1, n));
     y = y * GD_LCG_A + (GD_LCG_C << 16);
     const uint32_t r = (uint32_t)(y >> 33);
     rej |= r > rd.limit;
-    const int j = (int)(r - (__umulhi(r, rd.magic) >> rd.shift) * (uint32_t)n); /* r mod n, n >= 2 */
-    const uint8_t u = col[(n - 1) * PERM_ROW], v = col[j * PERM_ROW];
-    col[(n - 1) * PERM_ROW] = v;
-    col[j * PERM_ROW] = u;
+    return r - (__umulhi(r, rd.magic) >> rd.shift) * (uint32_t)n;
+  };
+  auto at = [&](uint32_t k) -> uint8_t * { return col + __umul24(k, (uint32_t)PERM_ROW); };
+#if PERM_FY_PIPE
+  if (m < 2) return false;
+  int n = __builtin_amdgcn_readfirstlane(m);
+  /* at the top of step n: jA = j_n with its reads (urA, vrA) in flight, jN = j_{n-1}
+   * drawn; step n issues the reads of step n - 1, draws j_{n-2}, then (the reads of
+   * step n now two draws old) forwards and writes.  sched_barrier keeps the compiler
+   * from hoisting the forwarding (and its wait) above the next reads and draw. */
+  uint32_t jA = draw(n);
+  uint8_t urA = *at((uint32_t)(n - 1)), vrA = *at(jA);
+  uint32_t jN = n > 2 ? draw(n - 1) : 0u;
+  uint32_t jp = 0xFFFFFFFFu; /* the previous step's j and u (none yet) */
+  uint8_t up = 0;
+#define FY_STEP(J, UR, V, URN, VRN, N)                                       \
+  do {                                                                      \
+    const uint32_t jn_ = jN;                                                \
+    URN = *at((uint32_t)((N) - 2));                                         \
+    VRN = *at(jn_);                                                         \
+    jN = draw((N) - 2);                                                     \
+    __builtin_amdgcn_sched_barrier(0);                                      \
+    const uint8_t u_ = jp == (uint32_t)((N) - 1) ? up : UR;                 \
+    const uint8_t v_ = jp == J ? up : V;                                    \
+    *at((uint32_t)((N) - 1)) = v_;                                          \
+    *at(J) = u_;                                                            \
+    jp = J;                                                                 \
+    up = u_;                                                                \
+    J = jn_;                                                                \
+  } while (0)
+  uint8_t urB, vrB;
+  for (; n > 4; n -= 2) { /* draws j_{n-2}, j_{n-3} >= 2 */
+    FY_STEP(jA, urA, vrA, urB, vrB, n);
+    FY_STEP(jA, urB, vrB, urA, vrA, n - 1);
   }
+#undef FY_STEP
+  { /* finish step n (2 <= n <= 4), then the last steps unpipelined */
+    const uint8_t u = jp == (uint32_t)(n - 1) ? up : urA, v = jp == jA ? up : vrA;
+    *at((uint32_t)(n - 1)) = v;
+    *at(jA) = u;
+  }
+  for (int k = n - 1; k >= 2; --k) {
+    const uint32_t j = k == n - 1 ? jN : draw(k);
+    const uint8_t u = *at((uint32_t)(k - 1)), v = *at(j);
+    *at((uint32_t)(k - 1)) = v;
+    *at(j) = u;
+  }
+#else
+  for (int s = 0; s < m - 1; ++s) {
+    const int n = __builtin_amdgcn_readfirstlane(m - s); /* wave-uniform */
+    const uint32_t j = draw(n);
+    const uint8_t u = *at((uint32_t)(n - 1)), v = *at(j);
+    *at((uint32_t)(n - 1)) = v;
+    *at(j) = u;
+  }
+#endif
   return rej;
 }
 
@@ -576,6 +651,86 @@ __device__ __forceinline__ void fy_exact(uint8_t *col, uint64_t x, int m, const 
     col[(n - 1) * PERM_ROW] = v;
     col[j * PERM_ROW] = u;
   }
+}
+
+
+/* sum over the wave, the same value in every lane (an xor butterfly: both lanes of a
+ * pair add the same two operands) */
+__device__ __forceinline__ double pw_sum(double v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+/* The exact FP64 css() (css.c:608-647) of one track array, computed by the whole wave
+ * (matrix-core tiers, <= 80 individuals): the observed score (identity tracks) and the
+ * rare permutations whose matrix-core estimate lies within its error bound of it.
+ *   consecutive within-group pairs (Q8): entry k = lane (and lane + 64) with entry k - 1;
+ *   between-group sum over the pairs (A_i, B_j) of the groups' members in ascending
+ *   order, pair p = i b + j dealt to lane p mod 64 and summed in p order per lane;
+ *   both reduced by the butterfly.
+ * A function of the order within each group and of the groups' SETS only, so every
+ * permutation that keeps them gets the observed value bit for bit (ties are decided
+ * identically for observed and permuted scores).  Distances from the coordinates
+ * (calc_dist, css.c:573-587; symmetric bit for bit).  ent(k): track entry k < m;
+ * lst: 256 bytes of the wave's LDS scratch; rb: random_int constants of n = b. */
+template <int MP, class ENT>
+__device__ double score_exact_wave(ENT ent, const double *X, int a, int b, double inva, double invb, int lane,
+                                   uint8_t *lst, const gd_randint &rb) {
+  static_assert(MP <= 80, "score_exact_wave's scratch holds 80 individuals per list");
+  const int m = a + b;
+  const uint32_t t0 = lane < m ? ent(lane) : 0u;
+  const uint32_t t1 = (MP > 64 && lane + 64 < m) ? ent(lane + 64) : 0u;
+  double wa = 0.0, wb = 0.0;
+  {
+    const uint32_t p0 = (uint32_t)__shfl_up((int)t0, 1);
+    const int k = lane;
+    if (k >= 1 && k < m && k != a) {
+      const double e = perm_xdist(X, (int)p0, (int)t0);
+      if (k < a)
+        wa = e;
+      else
+        wb = e;
+    }
+  }
+  if constexpr (MP > 64) {
+    const uint32_t s63 = (uint32_t)__shfl((int)t0, 63), su = (uint32_t)__shfl_up((int)t1, 1);
+    const uint32_t p1 = lane == 0 ? s63 : su;
+    const int k = lane + 64;
+    if (k < m && k != a) {
+      const double e = perm_xdist(X, (int)p1, (int)t1);
+      if (k < a)
+        wa += e;
+      else
+        wb += e;
+    }
+  }
+  wa = pw_sum(wa);
+  wb = pw_sum(wb);
+  /* membership flags (LDS in issue order within the wave), then the members ascending:
+   * rank = set lanes below in the ballot */
+  uint8_t *fl = lst, *la = lst + 96, *lb = lst + 176;
+  if (lane < m) fl[t0] = (uint8_t)(lane < a);
+  if (MP > 64 && lane + 64 < m) fl[t1] = (uint8_t)(lane + 64 < a);
+  __builtin_amdgcn_wave_barrier();
+  const bool v0 = lane < m, v1 = MP > 64 && lane + 64 < m;
+  const bool in0 = v0 && fl[lane] != 0, in1 = v1 && fl[(MP > 64 ? lane + 64 : lane)] != 0;
+  const uint64_t A0 = __ballot(in0), A1 = __ballot(in1), B0 = __ballot(v0 && !in0), B1 = __ballot(v1 && !in1);
+  const uint64_t below = (1ull << lane) - 1ull;
+  if (in0) la[__popcll(A0 & below)] = (uint8_t)lane;
+  if (v0 && !in0) lb[__popcll(B0 & below)] = (uint8_t)lane;
+  if (in1) la[__popcll(A0) + __popcll(A1 & below)] = (uint8_t)(lane + 64);
+  if (v1 && !in1) lb[__popcll(B0) + __popcll(B1 & below)] = (uint8_t)(lane + 64);
+  __builtin_amdgcn_wave_barrier();
+  double bet = 0.0;
+  const int nab = a * b;
+  for (int p = lane; p < nab; p += 64) {
+    const uint32_t i = b == 1 ? (uint32_t)p : (__umulhi((uint32_t)p, rb.magic) >> rb.shift);
+    const uint32_t j = (uint32_t)p - i * (uint32_t)b;
+    bet += perm_xdist(X, la[i], lb[j]);
+  }
+  bet = pw_sum(bet);
+  return bet / (double)(a * b) - (double)(a + b) * (wa * inva + wb * invb);
 }
 
 }  // namespace
@@ -599,8 +754,8 @@ __global__ void __launch_bounds__(PermShape<MP>::NT) PERM_WPE
   __shared__ double s_R[MP + 1];
   __shared__ uint64_t s_hit[NWV];
   __shared__ uint8_t s_car[MP > 64 ? 128 : 64];
-  __shared__ uint8_t s_gend[NWV * MP]; /* each wave's last composition */
-  __shared__ uint8_t s_fs[NWV * MP];   /* wave v > 0: the tracks before its first permutation */
+  __shared__ uint8_t s_gend[NWV * PERM_CHAINS * MP]; /* each chain's last composition */
+  __shared__ uint8_t s_fs[NWV * PERM_CHAINS * MP];   /* each chain's map: the tracks before its first permutation */
   __shared__ int64_t s_w;
   double *s_S = reinterpret_cast<double *>(s_U); /* FP64 triangle: window setup only */
   float *s_S32 = reinterpret_cast<float *>(s_U);  /* FP32 triangle: the permutation passes */
@@ -612,10 +767,19 @@ __global__ void __launch_bounds__(PermShape<MP>::NT) PERM_WPE
   if (tid < 16) /* fp16 1.0 = 0x3C00 */
     s_lut[tid] = make_uint2((tid & 1 ? 0x3C00u : 0u) | (tid & 2 ? 0x3C000000u : 0u),
                             (tid & 4 ? 0x3C00u : 0u) | (tid & 8 ? 0x3C000000u : 0u));
+  __syncthreads();
+  /* the magic numbers in VGPR lanes for fy_fast (kept for the kernel's life; the opaque
+   * use completes the loads here, so the draw loop carries no LDS wait for them) */
+  uint32_t vm0 = lane <= MP ? s_mag[lane] : 0u, vm1 = lane + 64 <= MP ? s_mag[lane + 64] : 0u;
+  PERM_OPAQUE(vm0);
+  PERM_OPAQUE(vm1);
   const char *s16 = s_U; /* score_mfma: the scaled fp16 matrix */
-  __shared__ unsigned long long s_smax; /* largest S entry of the window (bits of a non-negative double) */
   uint8_t *my_sig = reinterpret_cast<uint8_t *>(s_U + SH::OFF_SIG) + wave * SIG;
   uint8_t *my_mem = reinterpret_cast<uint8_t *>(s_U + SH::OFF_MEM) + wave * SH::MEM;
+  /* score_exact_wave's scratch (matrix-core tiers): 256 bytes per wave over the serial
+   * start states, which are dead outside the draw phase */
+  uint8_t *my_lst = reinterpret_cast<uint8_t *>(s_U + SH::OFF_MEM) + wave * 256;
+  static_assert(!SH::MF || NWV * 256 <= SH::MEMB, "score_exact_wave scratch");
 
   PERM_PROF_INIT;
   for (;;) {
@@ -630,81 +794,37 @@ __global__ void __launch_bounds__(PermShape<MP>::NT) PERM_WPE
     const int a = d.asize, b = d.bsize, m = a + b, m1 = m - 1;
     const int64_t wl = w - d.w_base;
 
-    /* S (packed triangle, zero rows for individuals >= m) and its row sums */
-    int ln = tid;
-    PERM_OPAQUE(ln);
-    for (int e = ln; e < 2 * m; e += NT) s_X[e] = xbuf[w * 2 * MP + e];
-    if (tid == 0) s_smax = 0ull;
-    __syncthreads();
-    /* entry e = T(h) + l of the triangle, e strided over the threads (independent
-     * entries, no per-row loop): h from the float root of 8e + 1 (within one of the
-     * true row for e < 2^24), then corrected */
-    double vmax = 0.0;
-#pragma unroll 4
-    for (int e = ln; e < TRI - 1; e += NT) {
-      int h = (int)((1.0f + __fsqrt_rn(8.0f * (float)e + 1.0f)) * 0.5f);
-      if (h * (h - 1) / 2 > e)
-        --h;
-      else if (h * (h + 1) / 2 <= e)
-        ++h;
-      const int l = e - h * (h - 1) / 2;
-      const double v = (h < m && l < m) ? perm_xdist(s_X, h, l) : 0.0;
-      s_S[e] = v;
-      vmax = fmax(vmax, v);
-    }
-    if (tid == 0) s_S[TRI - 1] = 0.0;
-    if constexpr (SH::MF) { /* the window's largest S entry (v >= 0: the bits order as the values) */
-#pragma unroll
-      for (int o = 32; o >= 1; o >>= 1) vmax = fmax(vmax, __shfl_xor(vmax, o));
-      if (lane == 0 && vmax > 0.0) atomicMax(&s_smax, (unsigned long long)__double_as_longlong(vmax));
-    }
-    __syncthreads();
-    for (int r = ln; r <= MP; r += NT) {
-      double acc = 0.0;
-      if (r < m) {
-        const uint32_t tr = tri8((uint32_t)r);
-        /* j ascending, eight loads in flight */
-#pragma unroll 1
-        for (int j0 = 0; j0 < m; j0 += 8) {
-          double e[8];
-#pragma unroll
-          for (int t = 0; t < 8; ++t) {
-            const int j = j0 + t;
-            e[t] = j < m ? s_pair(s_S, (uint32_t)r, tr, (uint32_t)j, tri8((uint32_t)j)) : 0.0;
-          }
-#pragma unroll
-          for (int t = 0; t < 8; ++t)
-            if (j0 + t < m && j0 + t != r) acc += e[t];
-        }
-      }
-      s_R[r] = acc;
-    }
-    if (tid < m) s_car[tid] = (uint8_t)tid; /* tracks := identity */
-    __syncthreads();
-
     const double inva = a > 1 ? 1.0 / (double)(a * a * (a - 1)) : 0.0;
     const double invb = b > 1 ? 1.0 / (double)(b * b * (b - 1)) : 0.0;
-    /* the observed score: identity tracks, from the FP64 triangle */
     const int g = a <= b ? a : b, goff = a <= b ? 0 : a;
-    const double obs = score_exact<MP, true>(
-        [](int k) { return (uint32_t)k; },
-        [&](int k) { return k < g ? (uint32_t)(goff + k) : (uint32_t)MP; },
-        [&](uint32_t x, uint32_t y) {
-          return *reinterpret_cast<const double *>(reinterpret_cast<const char *>(s_S) + tri8(y) + (x << 3));
-        },
-        s_R, a, b, inva, invb);
-    double inv_sc = 1.0; /* score_mfma: S was scaled by 1 / inv_sc */
+    double obs, inv_sc = 1.0; /* score_mfma: S was scaled by 1 / inv_sc */
+    int ln = tid;
+    PERM_OPAQUE(ln);
     if constexpr (SH::MF) {
-      /* the scaled fp16 matrix of S over region U (the FP64 triangle is dead once every
-       * thread has its obs): entry (row, k) from the coordinates, the same value the
-       * triangle held, times 2^(15 - e) for the largest entry's binary exponent e; zero
-       * outside m x m and on the diagonal */
-      const double smax = __longlong_as_double((long long)s_smax);
+      /* matrix-core tiers: no FP64 triangle.  The scale from the coordinates' bounding
+       * box (its diagonal D >= every distance, D < 2^ex), then the scaled fp16 matrix of
+       * S, zero outside m x m and on the diagonal, and the observed score by the wave */
+      for (int e = ln; e < 2 * m; e += NT) s_X[e] = xbuf[w * 2 * MP + e];
+      __syncthreads();
+      double x0 = __builtin_inf(), x1 = -__builtin_inf(), y0 = __builtin_inf(), y1 = -__builtin_inf();
+      for (int i = lane; i < m; i += 64) {
+        x0 = fmin(x0, s_X[2 * i]);
+        x1 = fmax(x1, s_X[2 * i]);
+        y0 = fmin(y0, s_X[2 * i + 1]);
+        y1 = fmax(y1, s_X[2 * i + 1]);
+      }
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) {
+        x0 = fmin(x0, __shfl_xor(x0, o));
+        x1 = fmax(x1, __shfl_xor(x1, o));
+        y0 = fmin(y0, __shfl_xor(y0, o));
+        y1 = fmax(y1, __shfl_xor(y1, o));
+      }
+      const double dmax = sqrt((x1 - x0) * (x1 - x0) + (y1 - y0) * (y1 - y0));
       int ex = 0;
-      if (smax > 0.0) (void)frexp(smax, &ex);
+      if (dmax > 0.0) (void)frexp(dmax, &ex);
       const double sc = ldexp(1.0, 15 - ex);
       inv_sc = ldexp(1.0, ex - 15);
-      __syncthreads();
       /* in FP32 (fp16 keeps 11 bits: the FP32 distance's ~2^-22 is inside the bound) */
       const float scf = (float)sc;
       constexpr int KC = SH::KT * 16;
@@ -717,27 +837,81 @@ __global__ void __launch_bounds__(PermShape<MP>::NT) PERM_WPE
         }
         *reinterpret_cast<_Float16 *>(s_U + row * SH::RS + 2 * k) = (_Float16)v;
       }
+      const gd_randint rb = perm_rd((uint32_t)(b > 1 ? b : 2), s_mag[b > 1 ? b : 2]);
+      obs = score_exact_wave<MP>([](int k) { return (uint32_t)k; }, s_X, a, b, inva, invb, lane, my_lst, rb);
+      if (tid < m) s_car[tid] = (uint8_t)tid; /* tracks := identity */
       __syncthreads();
-    } else
-    /* FP32 copy of the triangle over the head of the FP64 one, in chunks (the FP32
-     * entries of chunk j overlap only FP64 entries of chunks <= j, read before) */
-    {
-      constexpr int CH = 8;
+    } else {
+      /* S (packed triangle, zero rows for individuals >= m) and its row sums */
+      for (int e = ln; e < 2 * m; e += NT) s_X[e] = xbuf[w * 2 * MP + e];
+      __syncthreads();
+      /* entry e = T(h) + l of the triangle, e strided over the threads (independent
+       * entries, no per-row loop): h from the float root of 8e + 1 (within one of the
+       * true row for e < 2^24), then corrected */
+      #pragma unroll 4
+      for (int e = ln; e < TRI - 1; e += NT) {
+        int h = (int)((1.0f + __fsqrt_rn(8.0f * (float)e + 1.0f)) * 0.5f);
+        if (h * (h - 1) / 2 > e)
+          --h;
+        else if (h * (h + 1) / 2 <= e)
+          ++h;
+        const int l = e - h * (h - 1) / 2;
+        const double v = (h < m && l < m) ? perm_xdist(s_X, h, l) : 0.0;
+        s_S[e] = v;
+      }
+      if (tid == 0) s_S[TRI - 1] = 0.0;
+      __syncthreads();
+      for (int r = ln; r <= MP; r += NT) {
+        double acc = 0.0;
+        if (r < m) {
+          const uint32_t tr = tri8((uint32_t)r);
+          /* j ascending, eight loads in flight */
 #pragma unroll 1
-      for (int e0 = 0; e0 < TRI; e0 += CH * NT) {
-        float v[CH];
+          for (int j0 = 0; j0 < m; j0 += 8) {
+            double e[8];
 #pragma unroll
-        for (int i = 0; i < CH; ++i) {
-          const int e = e0 + i * NT + ln;
-          v[i] = e < TRI ? (float)s_S[e] : 0.f;
-        }
-        __syncthreads();
+            for (int t = 0; t < 8; ++t) {
+              const int j = j0 + t;
+              e[t] = j < m ? s_pair(s_S, (uint32_t)r, tr, (uint32_t)j, tri8((uint32_t)j)) : 0.0;
+            }
 #pragma unroll
-        for (int i = 0; i < CH; ++i) {
-          const int e = e0 + i * NT + ln;
-          if (e < TRI) s_S32[e] = v[i];
+            for (int t = 0; t < 8; ++t)
+              if (j0 + t < m && j0 + t != r) acc += e[t];
+          }
         }
-        __syncthreads();
+        s_R[r] = acc;
+      }
+      if (tid < m) s_car[tid] = (uint8_t)tid; /* tracks := identity */
+      __syncthreads();
+
+      /* the observed score: identity tracks, from the FP64 triangle */
+      obs = score_exact<MP, true>(
+          [](int k) { return (uint32_t)k; },
+          [&](int k) { return k < g ? (uint32_t)(goff + k) : (uint32_t)MP; },
+          [&](uint32_t x, uint32_t y) {
+            return *reinterpret_cast<const double *>(reinterpret_cast<const char *>(s_S) + tri8(y) + (x << 3));
+          },
+          s_R, a, b, inva, invb);
+      /* FP32 copy of the triangle over the head of the FP64 one, in chunks (the FP32
+       * entries of chunk j overlap only FP64 entries of chunks <= j, read before) */
+      {
+        constexpr int CH = 8;
+#pragma unroll 1
+        for (int e0 = 0; e0 < TRI; e0 += CH * NT) {
+          float v[CH];
+#pragma unroll
+          for (int i = 0; i < CH; ++i) {
+            const int e = e0 + i * NT + ln;
+            v[i] = e < TRI ? (float)s_S[e] : 0.f;
+          }
+          __syncthreads();
+#pragma unroll
+          for (int i = 0; i < CH; ++i) {
+            const int e = e0 + i * NT + ln;
+            if (e < TRI) s_S32[e] = v[i];
+          }
+          __syncthreads();
+        }
       }
     }
     PERM_PROF(0);
@@ -749,12 +923,12 @@ __global__ void __launch_bounds__(PermShape<MP>::NT) PERM_WPE
     while (!done) {
       /* 1. draws and Fisher-Yates swaps on sigma_q, q = tid */
       __syncthreads();
-      sig_identity(my_sig, m, lane);
+      sig_identity<MP>(my_sig, m, lane);
       __syncthreads();
       int lq = lane;
       PERM_OPAQUE(lq);
       uint8_t *col = my_sig + lq;
-      const bool rej = fy_fast(col, gd_affine_apply(Jq, base), m, s_mag);
+      const bool rej = fy_fast(col, gd_affine_apply(Jq, base), m, vm0, vm1);
       if (__syncthreads_or(rej)) {
         /* exact serial stream: the start state of every permutation of the pass */
         if (tid == 0) {
@@ -770,7 +944,7 @@ __global__ void __launch_bounds__(PermShape<MP>::NT) PERM_WPE
           s_st[P] = y;
         }
         __syncthreads();
-        sig_identity(my_sig, m, lane);
+        sig_identity<MP>(my_sig, m, lane);
         __syncthreads();
         fy_exact(col, s_st[tid], m, s_mag);
         base = s_st[P];
@@ -780,66 +954,86 @@ __global__ void __launch_bounds__(PermShape<MP>::NT) PERM_WPE
       __syncthreads();
       PERM_PROF(1);
 
-      /* 2. compositions, all waves at once; lane i owns rows i and i + 64.  Wave 0 composes
-       * F_q = F_{q-1} o sigma_q from the carried tracks; wave v > 0 composes
-       * G_t = G_{t-1} o sigma_{64v+t} from the identity, and its tracks are
-       * F_{64v+t} = Fs_v o G_t with Fs_v = F_{64v-1}, read through the map s_fs[v] */
+      /* 2. compositions, all waves at once; lane i owns rows i and i + 64.  The wave's 64
+       * permutations form PERM_CHAINS chains of consecutive ones (chain u = CH v + c holds
+       * q = 64 v + (64 / CH) c + t), composed side by side: with PERM_CHAINS == 1 wave 0
+       * composes F_q = F_{q-1} o sigma_q from the carried tracks and wave v > 0 composes
+       * G_t = G_{t-1} o sigma_{64v+t} from the identity, its tracks F_{64v+t} = Fs_v o G_t
+       * read through the map s_fs[v]; with PERM_CHAINS == 2 every chain starts from the
+       * identity and every lane reads through its chain's map (Fs_0 = the carried tracks),
+       * which halves the chain of dependent ds_bpermutes */
       {
+        constexpr int CH = PERM_CHAINS, TL = 64 / CH;
         uint32_t pf0[16], pf1[16];
         int li = lane;
         PERM_OPAQUE(li);
         const bool r0 = li < m, r1 = MP > 64 && li + 64 < m;
         /* above 64 individuals lane i carries F(i) and F(i + 64) as the low two bytes of
          * one word, so one ds_bpermute per row fetches whichever of the two is wanted */
-        uint32_t car = wave == 0 ? (uint32_t)s_car[li] | (MP > 64 ? (uint32_t)s_car[li + 64] << 8 : 0u)
-                                 : (uint32_t)li | (MP > 64 ? (uint32_t)(li + 64) << 8 : 0u);
+        const uint32_t ident = (uint32_t)li | (MP > 64 ? (uint32_t)(li + 64) << 8 : 0u);
+        uint32_t car[CH];
+#pragma unroll
+        for (int c = 0; c < CH; ++c) car[c] = ident;
+        if (CH == 1 && wave == 0) car[0] = (uint32_t)s_car[li] | (MP > 64 ? (uint32_t)s_car[li + 64] << 8 : 0u);
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
           pf0[q] = r0 ? *reinterpret_cast<const uint32_t *>(my_sig + li * PERM_ROW + 4 * q) : 0u;
           pf1[q] = r1 ? *reinterpret_cast<const uint32_t *>(my_sig + (li + 64) * PERM_ROW + 4 * q) : 0u;
         }
         /* F_q(i) for q = t .. t+3 leave as one dword per row (bytes t .. t+3 of row i) */
-        uint32_t w0 = 0, w1 = 0;
+        uint32_t w0[CH], w1[CH];
 #pragma unroll
-        for (int t = 0; t < 64; ++t) {
-          const uint32_t s0 = (pf0[t >> 2] >> (8 * (t & 3))) & 0xFFu;
-          uint32_t n0, n1 = 0;
-          if constexpr (MP > 64) {
-            const uint32_t s1 = (pf1[t >> 2] >> (8 * (t & 3))) & 0xFFu;
-            const uint32_t a0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((s0 & 63u) << 2), (int)car);
-            const uint32_t a1 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((s1 & 63u) << 2), (int)car);
-            n0 = (s0 < 64 ? a0 : a0 >> 8) & 0xFFu;
-            n1 = (s1 < 64 ? a1 : a1 >> 8) & 0xFFu;
-            w1 |= n1 << (8 * (t & 3));
-          } else {
-            n0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(s0 << 2), (int)car);
+        for (int c = 0; c < CH; ++c) w0[c] = w1[c] = 0u;
+#pragma unroll
+        for (int t = 0; t < TL; ++t) {
+#pragma unroll
+          for (int c = 0; c < CH; ++c) {
+            const int q = TL * c + t;
+            const uint32_t s0 = (pf0[q >> 2] >> (8 * (q & 3))) & 0xFFu;
+            uint32_t n0, n1 = 0;
+            if constexpr (MP > 64) {
+              const uint32_t s1 = (pf1[q >> 2] >> (8 * (q & 3))) & 0xFFu;
+              const uint32_t a0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((s0 & 63u) << 2), (int)car[c]);
+              const uint32_t a1 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((s1 & 63u) << 2), (int)car[c]);
+              n0 = (s0 < 64 ? a0 : a0 >> 8) & 0xFFu;
+              n1 = (s1 < 64 ? a1 : a1 >> 8) & 0xFFu;
+              w1[c] |= n1 << (8 * (q & 3));
+            } else {
+              n0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(s0 << 2), (int)car[c]);
+            }
+            w0[c] |= n0 << (8 * (q & 3));
+            if ((q & 3) == 3) {
+              if (r0) *reinterpret_cast<uint32_t *>(my_sig + li * PERM_ROW + (q & ~3)) = w0[c];
+              if (MP > 64 && r1) *reinterpret_cast<uint32_t *>(my_sig + (li + 64) * PERM_ROW + (q & ~3)) = w1[c];
+              w0[c] = 0;
+              w1[c] = 0;
+            }
+            car[c] = n0 | (n1 << 8);
           }
-          w0 |= n0 << (8 * (t & 3));
-          if ((t & 3) == 3) {
-            if (r0) *reinterpret_cast<uint32_t *>(my_sig + li * PERM_ROW + (t & ~3)) = w0;
-            if (MP > 64 && r1) *reinterpret_cast<uint32_t *>(my_sig + (li + 64) * PERM_ROW + (t & ~3)) = w1;
-            w0 = 0;
-            w1 = 0;
-          }
-          car = n0 | (n1 << 8);
         }
-        /* the wave's last composition: F_{63} (wave 0) or G_{63} (wave v > 0) */
-        uint8_t *gend = s_gend + wave * MP;
-        if (r0) gend[li] = (uint8_t)car;
-        if (r1) gend[li + 64] = (uint8_t)(car >> 8);
+        /* each chain's last composition */
+#pragma unroll
+        for (int c = 0; c < CH; ++c) {
+          uint8_t *gend = s_gend + (CH * wave + c) * MP;
+          if (r0) gend[li] = (uint8_t)car[c];
+          if (r1) gend[li + 64] = (uint8_t)(car[c] >> 8);
+        }
       }
       __syncthreads();
-      /* the chain across the waves: Fs_1 = F_63, Fs_v = Fs_{v-1} o G^{v-1}_63, and the
-       * carry into the next pass Fs_{NWV-1} o G^{NWV-1}_63 (NWV - 1 small compositions) */
+      /* the chain across the chains, wave 0 alone (LDS in issue order: each step reads what
+       * the previous one wrote).  PERM_CHAINS == 1: Fs_1 = F_63, Fs_v = Fs_{v-1} o G^{v-1}_63;
+       * PERM_CHAINS == 2: Fs_0 = the carried tracks, Fs_u = Fs_{u-1} o G^{u-1}_end.  The carry
+       * into the next pass is the last map composed with the last chain's end. */
       if (wave == 0) {
-        /* wave 0 alone, LDS in issue order: each step reads what the previous one wrote */
-        for (int v = 1; v < NWV; ++v) {
+        constexpr int NCH = NWV * PERM_CHAINS, U0 = PERM_CHAINS == 1 ? 1 : 0;
+        for (int u = U0; u < NCH; ++u) {
           for (int i = lane; i < m; i += 64)
-            s_fs[v * MP + i] = v == 1 ? s_gend[i] : s_fs[(v - 1) * MP + s_gend[(v - 1) * MP + i]];
+            s_fs[u * MP + i] = u == 0 ? s_car[i] : (U0 == 1 && u == 1) ? s_gend[i]
+                                                                        : s_fs[(u - 1) * MP + s_gend[(u - 1) * MP + i]];
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         }
         for (int i = lane; i < m; i += 64)
-          s_car[i] = NWV == 1 ? s_gend[i] : s_fs[(NWV - 1) * MP + s_gend[(NWV - 1) * MP + i]];
+          s_car[i] = NCH == 1 ? s_gend[i] : s_fs[(NCH - 1) * MP + s_gend[(NCH - 1) * MP + i]];
       }
       __syncthreads();
       PERM_PROF(2);
@@ -852,15 +1046,11 @@ __global__ void __launch_bounds__(PermShape<MP>::NT) PERM_WPE
       const uint8_t *tcol = my_sig + lc;
       uint8_t *mcol = my_mem + lc;
       double est, err;
-      const bool mapped = __builtin_amdgcn_readfirstlane(wave) > 0;
-      const uint8_t *fmap = s_fs + __builtin_amdgcn_readfirstlane(wave) * MP;
-      uint64_t glo = 0, ghi = 0; /* the smaller group's members (score_mfma) */
+      /* the lane's chain map (PERM_CHAINS == 1: wave-uniform, none for wave 0) */
+      const bool mapped = PERM_CHAINS > 1 || __builtin_amdgcn_readfirstlane(wave) > 0;
+      const uint8_t *fmap = s_fs + (PERM_CHAINS * wave + lc / (64 / PERM_CHAINS)) * MP;
       if constexpr (SH::MF) {
-        uint64_t alo, ahi;
-        score_mfma<MP>(s16, s_lut, tcol, fmap, mapped, a, b, inva, invb, inv_sc, lane, est, err, alo, ahi);
-        const uint64_t vlo = m >= 64 ? ~0ull : ((1ull << m) - 1), vhi = m > 64 ? ((1ull << (m - 64)) - 1) : 0ull;
-        glo = a <= b ? alo : ~alo & vlo;
-        ghi = a <= b ? ahi : ~ahi & vhi;
+        score_mfma<MP>(s16, s_lut, tcol, fmap, mapped, a, b, inva, invb, inv_sc, lane, est, err);
       } else {
         score_f32<MP>(s_S32, s_R, tcol, fmap, mapped, mcol, a, b, inva, invb, est, err);
       }
@@ -870,19 +1060,33 @@ __global__ void __launch_bounds__(PermShape<MP>::NT) PERM_WPE
       if (hit < 0) atomicAdd(&g_perm_amb[0], 1ull);
       if (__any(hit < 0) && lane == 0) atomicAdd(&g_perm_amb[1], 1ull);
 #endif
-      if (__any(hit < 0)) {
+      if constexpr (SH::MF) {
+        /* the rare lanes inside the bound: exact score by the whole wave, one lane at a time */
+        uint64_t amb = __ballot(hit < 0);
+        if (amb) {
+          const gd_randint rb = perm_rd((uint32_t)(b > 1 ? b : 2), s_mag[b > 1 ? b : 2]);
+          while (amb) {
+            const int L = __builtin_ctzll(amb);
+            amb &= amb - 1;
+            const uint8_t *cl = my_sig + L;
+            const uint8_t *fmL = s_fs + (PERM_CHAINS * wave + L / (64 / PERM_CHAINS)) * MP;
+            const double sc = score_exact_wave<MP>(
+                [&](int k) {
+                  const uint32_t c = cl[k * PERM_ROW];
+                  return mapped ? (uint32_t)fmL[c] : c;
+                },
+                s_X, a, b, inva, invb, lane, my_lst, rb);
+            if (lane == L) hit = sc >= obs;
+          }
+        }
+      } else if (__any(hit < 0)) {
         if (hit < 0) {
           const double sc = score_exact<MP, false>(
               [&](int k) {
                 const uint32_t c = tcol[k * PERM_ROW];
                 return mapped ? (uint32_t)fmap[c] : c;
               },
-              [&](int k) {
-                if constexpr (SH::MF)
-                  return k < g ? pm_kth_bit(glo, ghi, k) : (uint32_t)MP;
-                else
-                  return k < g ? (uint32_t)mcol[k * 64] : (uint32_t)MP;
-              },
+              [&](int k) { return k < g ? (uint32_t)mcol[k * 64] : (uint32_t)MP; },
               [&](uint32_t x, uint32_t y) { return y < (uint32_t)m ? perm_xdist(s_X, (int)y, (int)x) : 0.0; }, s_R,
               a, b, inva, invb);
           hit = sc >= obs;
