@@ -625,13 +625,20 @@ __device__ __forceinline__ bool fy_fast(uint8_t *col, uint64_t x, int m, uint32_
     *at(j) = u;
   }
 #else
-  for (int s = 0; s < m - 1; ++s) {
-    const int n = __builtin_amdgcn_readfirstlane(m - s); /* wave-uniform */
-    const uint32_t j = draw(n);
+  /* steps n >= 64 read their magic from vm1, the rest from vm0: one readlane per step */
+  auto step = [&](int n, uint32_t mg) {
+    const gd_randint rd = perm_rd((uint32_t)n, mg);
+    y = y * GD_LCG_A + (GD_LCG_C << 16);
+    const uint32_t r = (uint32_t)(y >> 33);
+    rej |= r > rd.limit;
+    const uint32_t j = r - (__umulhi(r, rd.magic) >> rd.shift) * (uint32_t)n;
     const uint8_t u = *at((uint32_t)(n - 1)), v = *at(j);
     *at((uint32_t)(n - 1)) = v;
     *at(j) = u;
-  }
+  };
+  int n = __builtin_amdgcn_readfirstlane(m);
+  for (; n >= 64; --n) step(n, (uint32_t)__builtin_amdgcn_readlane((int)vm1, n - 64));
+  for (; n >= 2; --n) step(n, (uint32_t)__builtin_amdgcn_readlane((int)vm0, n));
 #endif
   return rej;
 }
@@ -989,14 +996,16 @@ __global__ void __launch_bounds__(PermShape<MP>::NT) PERM_WPE
 #pragma unroll
           for (int c = 0; c < CH; ++c) {
             const int q = TL * c + t;
-            const uint32_t s0 = (pf0[q >> 2] >> (8 * (q & 3))) & 0xFFu;
+            const uint32_t s0 = __builtin_amdgcn_ubfe(pf0[q >> 2], 8 * (q & 3), 8);
             uint32_t n0, n1 = 0;
             if constexpr (MP > 64) {
-              const uint32_t s1 = (pf1[q >> 2] >> (8 * (q & 3))) & 0xFFu;
-              const uint32_t a0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((s0 & 63u) << 2), (int)car[c]);
-              const uint32_t a1 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((s1 & 63u) << 2), (int)car[c]);
-              n0 = (s0 < 64 ? a0 : a0 >> 8) & 0xFFu;
-              n1 = (s1 < 64 ? a1 : a1 >> 8) & 0xFFu;
+              /* ds_bpermute reads lane (addr >> 2) mod 64; entry s >= 64 is byte 1 of lane
+               * s - 64's word: bit field (8 (s >> 6), 8) */
+              const uint32_t s1 = __builtin_amdgcn_ubfe(pf1[q >> 2], 8 * (q & 3), 8);
+              const uint32_t a0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(s0 << 2), (int)car[c]);
+              const uint32_t a1 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(s1 << 2), (int)car[c]);
+              n0 = __builtin_amdgcn_ubfe(a0, (s0 >> 3) & 8u, 8);
+              n1 = __builtin_amdgcn_ubfe(a1, (s1 >> 3) & 8u, 8);
               w1[c] |= n1 << (8 * (q & 3));
             } else {
               n0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(s0 << 2), (int)car[c]);
