@@ -543,6 +543,9 @@ __device__ __forceinline__ gd_randint perm_rd(uint32_t n, uint32_t magic) {
   return d;
 }
 
+#ifndef PERM_FY_UNROLL
+#define PERM_FY_UNROLL 1 /* Fisher-Yates steps unrolled with literal constants (fy_fast_unrolled) */
+#endif
 #ifndef PERM_FY_PIPE
 #define PERM_FY_PIPE 0 /* software-pipelined Fisher-Yates (reads one step ahead, forwarded): measured
                         * slower (the draw phase is issue-bound; forwarding adds 4 VALU per step) */
@@ -640,6 +643,55 @@ __device__ __forceinline__ bool fy_fast(uint8_t *col, uint64_t x, int m, uint32_
   for (; n >= 64; --n) step(n, (uint32_t)__builtin_amdgcn_readlane((int)vm1, n - 64));
   for (; n >= 2; --n) step(n, (uint32_t)__builtin_amdgcn_readlane((int)vm0, n));
 #endif
+  return rej;
+}
+
+/* random_int_nrand48 constants of a compile-time n (gd_randint_make's formulas) */
+struct PmRd {
+  uint32_t magic, shift, limit;
+};
+constexpr PmRd pm_rd_const(uint32_t n) {
+  uint32_t l = 0;
+  while ((1ull << l) < n) ++l;
+  PmRd d{0u, 0u, 0x7FFFFFFFu - (uint32_t)(0x80000000ull % n)};
+  if (l) {
+    d.magic = (uint32_t)(((1ull << (31 + l)) + n - 1) / n);
+    d.shift = l - 1;
+  }
+  return d;
+}
+
+/* fy_fast with every step unrolled (PERM_FY_UNROLL): step n's magic number, shift and
+ * rejection limit are literals and its row n - 1 an immediate LDS offset, so a step is
+ * the LCG, the remainder, one address and the swap -- no readlane, no scalar
+ * arithmetic.  Taken when the window fills its tier (m == MP, e.g. 40 + 40); other
+ * cohorts run the loop (fy_fast). */
+template <int N>
+__device__ __forceinline__ void fy_step(uint8_t *col, uint64_t &y, bool &rej) {
+  constexpr PmRd rd = pm_rd_const((uint32_t)N);
+  y = y * GD_LCG_A + (GD_LCG_C << 16);
+  const uint32_t r = (uint32_t)(y >> 33);
+  rej |= r > rd.limit;
+  const uint32_t j = r - (__umulhi(r, rd.magic) >> rd.shift) * (uint32_t)N;
+  uint8_t *pn = col + (N - 1) * PERM_ROW;
+  uint8_t *pj = col + __umul24(j, (uint32_t)PERM_ROW);
+  const uint8_t u = *pn, v = *pj;
+  *pn = v;
+  *pj = u;
+}
+template <int N>
+__device__ __forceinline__ void fy_steps(uint8_t *col, uint64_t &y, bool &rej) {
+  if constexpr (N >= 2) {
+    fy_step<N>(col, y, rej);
+    fy_steps<N - 1>(col, y, rej);
+  }
+}
+/* a full tier (m == MP): the steps n = MP .. 2 as one straight line */
+template <int MP>
+__device__ __forceinline__ bool fy_fast_unrolled(uint8_t *col, uint64_t x) {
+  bool rej = false;
+  uint64_t y = x << 16;
+  fy_steps<MP>(col, y, rej);
   return rej;
 }
 
@@ -935,7 +987,13 @@ __global__ void __launch_bounds__(PermShape<MP>::NT) PERM_WPE
       int lq = lane;
       PERM_OPAQUE(lq);
       uint8_t *col = my_sig + lq;
+#if PERM_FY_UNROLL
+      /* (not at 64: the straight line raised that tier's VGPRs 160 -> 196, 3 -> 2 waves per SIMD) */
+      const bool rej = (MP != 64 && m == MP) ? fy_fast_unrolled<MP>(col, gd_affine_apply(Jq, base))
+                                             : fy_fast(col, gd_affine_apply(Jq, base), m, vm0, vm1);
+#else
       const bool rej = fy_fast(col, gd_affine_apply(Jq, base), m, vm0, vm1);
+#endif
       if (__syncthreads_or(rej)) {
         /* exact serial stream: the start state of every permutation of the pass */
         if (tid == 0) {
