@@ -394,6 +394,7 @@ __device__ __forceinline__ void score_mfma(const char *s16, const uint2 *lut, co
   using SH = PermShape<MP>;
   constexpr int MT = SH::MT, KT = SH::KT, RS = SH::RS;
   static_assert(MP <= 96, "score_mfma keeps members 64.. in one 32-bit word");
+  static_assert(SH::MT <= 3, "score_mfma's row tiles take their mask words from (lo, hi)");
   const int m = a + b;
   uint64_t lo = 0, hi = 0;
   auto s_at = [&](uint32_t x, uint32_t y) -> float {
@@ -492,11 +493,15 @@ __device__ __forceinline__ void score_mfma(const char *s16, const uint2 *lut, co
         acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bf, acc, 0, 0, 0);
         if (kt & 1) asm volatile("" ::: "memory"); /* two k steps of fragment loads in flight */
       }
+      /* accumulator e holds row t * 32 + 4 h + (e & 3) + 8 (e >> 2) of this lane's column:
+       * its membership bit from the tile's 32-bit word of the A-mask, as an all-ones /
+       * zero mask (one sign-extending bit-field extract) ANDed into the float */
+      const uint32_t W = t == 0 ? (uint32_t)a0 : (t == 1 ? (uint32_t)(a0 >> 32) : (uint32_t)a1);
+      const uint32_t Wh = W >> (4 * h);
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
-        const int i = t * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
-        const uint64_t mk = i < 64 ? a0 >> i : a1 >> (i - 64);
-        part += (mk & 1u) ? acc[e] : 0.f;
+        const uint32_t msk = (uint32_t)__builtin_amdgcn_sbfe((int)Wh, (e & 3) + 8 * (e >> 2), 1);
+        part += __uint_as_float(__float_as_uint(acc[e]) & msk);
       }
     }
     if (n == h)
