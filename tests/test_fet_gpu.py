@@ -283,3 +283,39 @@ def test_golden_reference_fixtures(name):
     assert np.array_equal(s == 0, f["scores"] == 0)
     assert close(s, f["scores"]) and close(d, f["stddev"])
     assert np.mean(s == f["scores"]) > 0.99
+
+
+
+def _irregular(kind):
+    av, bv, ap, bp, regend = _synth(11, 9000, 10, 10)
+    ap, bp = ap.copy(), bp.copy()
+    if kind == "gaps":  # a 40 kb hole and a late start: windows with no SNP
+        ap[ap > 150_000] += 40_000
+        bp[bp > 150_000] += 40_000
+        ap += 3_000
+        bp += 3_000
+        regend = int(ap[-1]) + 1
+    elif kind == "stacked":  # runs of SNP rows sharing one position (the first row alone)
+        ap = (-(-ap // 700) * 700).astype(np.int32)
+        bp = (-(-bp // 700) * 700).astype(np.int32)
+        ap[:10] = 0
+        bp[:10] = 0
+        assert (ap[10:] > 0).all() and (bp[10:] > 0).all()
+    elif kind == "misaligned":  # B one row ahead of A
+        bv = np.concatenate([np.full(10, 3.0), bv])
+        bp = np.concatenate([np.zeros(10, np.int32), bp])
+    return av, bv, ap, bp, regend
+
+
+@pytest.mark.parametrize("kind,wsize,wstep", [("gaps", 2500, 500), ("stacked", 2500, 500), ("misaligned", 2500, 500),
+                                              ("plain", 2500, 250), ("plain", 1000, 500)])
+def test_irregular_geometries(oracle, kind, wsize, wstep):
+    """Window bounds (slide_right, comparative.c:49-71) on gaps (windows without SNPs, a
+    late first position), runs of rows sharing a position, B one row ahead of A, and other
+    window geometries: the device scan equals the oracle."""
+    from gdscan import fet
+    av, bv, ap, bp, regend = _irregular(kind)
+    s, d = fet.scan(av, bv, ap, bp, regend, wsize, wstep, seed=5)
+    s_ref, d_ref = oracle_fet_scan(oracle, av, bv, ap, bp, regend, wsize, wstep, seed=5)
+    assert (s_ref != 0).sum() > 50 and np.isfinite(s_ref).mean() > 0.9
+    assert close(s, s_ref) and close(d, d_ref)
