@@ -262,6 +262,8 @@ def test_serial_window_set_with_permutations(oracle):
                                                                 (40, 40, 10, 1000, 3_000, True),
                                                                 (20, 20, 100_000, 400, 6_000, True),
                                                                 (45, 45, 100_000, 200, 1_800, False),
+                                                                (12, 12, 100_000, 300, 8_000, False),
+                                                                (48, 48, 100_000, 100, 1_600, False),
                                                                 (64, 64, 100_000, 100, 1_400, True)])
 def test_fp32_prefilter_changes_no_p(asize, bsize, treshold, runs, nsnp, dup, monkeypatch):
     """The permutation kernel decides hits from an estimate -- the matrix-core score

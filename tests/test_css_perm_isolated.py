@@ -74,12 +74,14 @@ def _check(orc, a, b, nsnp, treshold, runs, seed, chrom=5, dup=False, serial=Fal
 
 @pytest.mark.parametrize("a,b,nsnp,treshold,runs", [
     (10, 10, 12_000, 10, 300),   # tier 24
+    (12, 12, 10_000, 10, 300),   # tier 24 filled (m == MP: the straight-line Fisher-Yates)
     (12, 13, 6_000, 10, 300),    # p40 tier, m = 25
     (16, 17, 6_000, 10, 300),    # m = 33
     (20, 20, 6_000, 50, 400),    # m = 40, full runs and early exits
     (33, 31, 3_000, 10, 200),    # tier 64
     (40, 40, 2_500, 10, 1000),   # tier 80 (the C5 shape)
     (45, 45, 1_800, 10, 150),    # tier 96
+    (48, 48, 1_600, 10, 150),    # tier 96 filled (straight-line Fisher-Yates)
     (50, 47, 1_500, 20, 120),    # tier 128, m = 97: the 64-bit hi member word
     (64, 64, 1_400, 10, 100),    # tier 128, m = 128
     (1, 30, 6_000, 10, 300),     # a single individual in A (no within-A pairs)
@@ -90,7 +92,8 @@ def test_perm_on_device_coordinates(oracle, a, b, nsnp, treshold, runs):
     assert exact >= n - ties and ties <= max(1, n // 100), (n, exact, ties)
 
 
-@pytest.mark.parametrize("a,b,nsnp,runs", [(6, 9, 10_000, 1000), (40, 40, 2_500, 500), (45, 45, 1_800, 200)])
+@pytest.mark.parametrize("a,b,nsnp,runs", [(6, 9, 10_000, 1000), (12, 12, 8_000, 500), (40, 40, 2_500, 500),
+                                            (45, 45, 1_800, 200)])
 def test_perm_exact_ties(oracle, a, b, nsnp, runs):
     """Duplicated individuals make many permuted scores equal the observed one in exact
     arithmetic: p must still lie inside the tie bracket in every window."""
