@@ -114,68 +114,72 @@ __global__ void __launch_bounds__(256) k_bounds(const gd_chrom_dev *ch, const in
    * VALU per element: unsigned difference, min with 1, shift-or), then the lane walks
    * just those bits: a wave runs the window-range code max-boundaries-per-lane times
    * (~1-2 at 20 individuals), not once per element */
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x * 16;
+  /* a wave scans a 1024-element segment: lane l's chunk k holds elements seg + 256 k + 4 l
+   * .. + 3 (one coalesced int4 per chunk: consecutive lanes read consecutive 16 bytes);
+   * an element's predecessor is the previous element of its chunk, or the last element of
+   * lane l - 1's chunk (ds_bpermute), or of lane 63's previous chunk.  The partial last
+   * segment takes the element-by-element path (16 consecutive elements per lane). */
+  const int lane = threadIdx.x & 63;
+  const int64_t wave0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
   bool unsorted = false;
-  for (int64_t i0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 16; i0 <= len; i0 += stride) {
-    int32_t prev = (i0 > 0) ? pos[i0 - 1] : 0;
-    uint32_t bits = 0;
-    if (i0 + 16 <= len) {
-      int32_t v16[16];
-      if (aligned16) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const int4 t = *reinterpret_cast<const int4 *>(pos + i0 + 4 * k);
-          v16[4 * k] = t.x;
-          v16[4 * k + 1] = t.y;
-          v16[4 * k + 2] = t.z;
-          v16[4 * k + 3] = t.w;
-        }
-      } else {
-#pragma unroll
-        for (int k = 0; k < 16; ++k) v16[k] = pos[i0 + k];
-      }
-      bool dec = false;
-#pragma unroll
-      for (int k = 0; k < 16; ++k) {
-        const int32_t v = v16[k];
-        bits |= min((uint32_t)v - (uint32_t)prev, 1u) << k;
-        dec |= v < prev;
-        prev = v;
-      }
-      if (i0 == 0) {
-        bits |= 1u; /* element 0 opens the first run; it has no predecessor */
-        dec = false;
-#pragma unroll
-        for (int k = 1; k < 16; ++k) dec |= v16[k] < v16[k - 1];
-      }
-      unsorted |= dec;
-    } else {
-      for (int k = 0; k < 16 && i0 + k <= len; ++k) {
-        const int64_t i = i0 + k;
-        const int32_t v = (i < len) ? pos[i] : 0;
-        const bool bnd = (i == 0) || (i == len) || (v != prev);
-        if (i > 0 && i < len) unsorted |= (v < prev);
-        bits |= bnd ? 1u << k : 0u;
-        prev = v;
-      }
-    }
-    while (bits) {
-      const int64_t i = i0 + __builtin_ctz(bits);
-      bits &= bits - 1;
-      const bool first = (i == 0), last = (i == len);
-      const int64_t p = last ? 0 : pos[i];
-      const int64_t pp = first ? 0 : pos[i - 1];
-      int64_t f = first ? 0 : fdiv_fast(pp, wstep, inv) + 1;
-      int64_t l = last ? wend - 1 : fdiv_fast(p, wstep, inv);
+  auto own = [&](int64_t i) { /* element i (a boundary: i == 0, i == len or pos[i] != pos[i-1]) */
+    const bool first = (i == 0), last = (i == len);
+    const int64_t p = last ? 0 : pos[i];
+    const int64_t pp = first ? 0 : pos[i - 1];
+    int64_t f = first ? 0 : fdiv_fast(pp, wstep, inv) + 1;
+    int64_t l = last ? wend - 1 : fdiv_fast(p, wstep, inv);
+    if (f < 0) f = 0;
+    if (l > wend - 1) l = wend - 1;
+    for (int64_t w = f; w <= l; ++w) lo[w] = (int32_t)i;
+    if (pop == 0) {
+      f = first ? 0 : -fdiv_fast(wsize - pp, wstep, inv);
+      l = last ? wend - 1 : -fdiv_fast(wsize - p, wstep, inv) - 1;
       if (f < 0) f = 0;
       if (l > wend - 1) l = wend - 1;
-      for (int64_t w = f; w <= l; ++w) lo[w] = (int32_t)i;
-      if (pop == 0) {
-        f = first ? 0 : -fdiv_fast(wsize - pp, wstep, inv);
-        l = last ? wend - 1 : -fdiv_fast(wsize - p, wstep, inv) - 1;
-        if (f < 0) f = 0;
-        if (l > wend - 1) l = wend - 1;
-        for (int64_t w = f; w <= l; ++w) hi[w] = (int32_t)i;
+      for (int64_t w = f; w <= l; ++w) hi[w] = (int32_t)i;
+    }
+  };
+  for (int64_t seg = wave0 * 1024; seg <= len; seg += nwaves * 1024) {
+    if (aligned16 && seg + 1024 <= len) {
+      int4 v[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[k] = *reinterpret_cast<const int4 *>(pos + seg + 256 * k + 4 * lane);
+      const int32_t before = seg > 0 ? pos[seg - 1] : v[0].x; /* element 0 has no predecessor */
+      uint32_t bits = 0;
+      bool dec = false;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int32_t up = __shfl_up(v[k].w, 1);
+        const int32_t wrap = __shfl(v[k > 0 ? k - 1 : 0].w, 63);
+        const int32_t prev = lane > 0 ? up : (k > 0 ? wrap : before);
+        const int32_t e[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+        int32_t pv = prev;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          bits |= min((uint32_t)e[j] - (uint32_t)pv, 1u) << (4 * k + j);
+          dec |= e[j] < pv;
+          pv = e[j];
+        }
+      }
+      if (seg == 0 && lane == 0) bits |= 1u; /* element 0 opens the first run */
+      unsorted |= dec;
+      while (bits) {
+        const int b = __builtin_ctz(bits);
+        bits &= bits - 1;
+        own(seg + 256 * (b >> 2) + 4 * lane + (b & 3));
+      }
+    } else {
+      for (int64_t i0 = seg + 16 * lane; i0 < seg + 1024 && i0 <= len; i0 += 1024) {
+        int32_t prev = (i0 > 0) ? pos[i0 - 1] : 0;
+        for (int k = 0; k < 16 && i0 + k <= len; ++k) {
+          const int64_t i = i0 + k;
+          const int32_t v = (i < len) ? pos[i] : 0;
+          const bool bnd = (i == 0) || (i == len) || (v != prev);
+          if (i > 0 && i < len) unsorted |= (v < prev);
+          if (bnd) own(i);
+          prev = v;
+        }
       }
     }
   }
