@@ -114,11 +114,15 @@ __global__ void __launch_bounds__(256) k_bounds(const gd_chrom_dev *ch, const in
    * VALU per element: unsigned difference, min with 1, shift-or), then the lane walks
    * just those bits: a wave runs the window-range code max-boundaries-per-lane times
    * (~1-2 at 20 individuals), not once per element */
-  /* a wave scans a 1024-element segment: lane l's chunk k holds elements seg + 256 k + 4 l
+  /* a wave scans a KB_SEG-element segment (KB_CH chunks of 256): lane l's chunk k holds elements seg + 256 k + 4 l
    * .. + 3 (one coalesced int4 per chunk: consecutive lanes read consecutive 16 bytes);
    * an element's predecessor is the previous element of its chunk, or the last element of
    * lane l - 1's chunk (ds_bpermute), or of lane 63's previous chunk.  The partial last
    * segment takes the element-by-element path (16 consecutive elements per lane). */
+#ifndef KB_CH
+#define KB_CH 4 /* int4 chunks per lane and segment (loads in flight) */
+#endif
+  constexpr int KB_SEG = 256 * KB_CH;
   const int lane = threadIdx.x & 63;
   const int64_t wave0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
@@ -140,16 +144,16 @@ __global__ void __launch_bounds__(256) k_bounds(const gd_chrom_dev *ch, const in
       for (int64_t w = f; w <= l; ++w) hi[w] = (int32_t)i;
     }
   };
-  for (int64_t seg = wave0 * 1024; seg <= len; seg += nwaves * 1024) {
-    if (aligned16 && seg + 1024 <= len) {
-      int4 v[4];
+  for (int64_t seg = wave0 * KB_SEG; seg <= len; seg += nwaves * KB_SEG) {
+    if (aligned16 && seg + KB_SEG <= len) {
+      int4 v[KB_CH];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) v[k] = *reinterpret_cast<const int4 *>(pos + seg + 256 * k + 4 * lane);
+      for (int k = 0; k < KB_CH; ++k) v[k] = *reinterpret_cast<const int4 *>(pos + seg + 256 * k + 4 * lane);
       const int32_t before = seg > 0 ? pos[seg - 1] : v[0].x; /* element 0 has no predecessor */
       uint32_t bits = 0;
       bool dec = false;
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
+      for (int k = 0; k < KB_CH; ++k) {
         const int32_t up = __shfl_up(v[k].w, 1);
         const int32_t wrap = __shfl(v[k > 0 ? k - 1 : 0].w, 63);
         const int32_t prev = lane > 0 ? up : (k > 0 ? wrap : before);
@@ -170,9 +174,9 @@ __global__ void __launch_bounds__(256) k_bounds(const gd_chrom_dev *ch, const in
         own(seg + 256 * (b >> 2) + 4 * lane + (b & 3));
       }
     } else {
-      for (int64_t i0 = seg + 16 * lane; i0 < seg + 1024 && i0 <= len; i0 += 1024) {
+      for (int64_t i0 = seg + 4 * KB_CH * lane; i0 < seg + KB_SEG && i0 <= len; i0 += KB_SEG) {
         int32_t prev = (i0 > 0) ? pos[i0 - 1] : 0;
-        for (int k = 0; k < 16 && i0 + k <= len; ++k) {
+        for (int k = 0; k < 4 * KB_CH && i0 + k <= len; ++k) {
           const int64_t i = i0 + k;
           const int32_t v = (i < len) ? pos[i] : 0;
           const bool bnd = (i == 0) || (i == len) || (v != prev);
