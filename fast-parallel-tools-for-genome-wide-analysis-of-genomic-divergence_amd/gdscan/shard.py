@@ -46,14 +46,16 @@ def gather_tracks(local, shards, windows_per_chrom, group=None):
     dist.all_gather_into_tensor(out, buf, group=group)
     offs = np.concatenate([[0], np.cumsum([int(w) for w in windows_per_chrom])])
     total = int(offs[-1])
-    track = torch.empty((total, width), dtype=local.dtype, device=local.device)
+    # one gather into genome order: row offs[c] + k of the track is row r * pad + pos_c + k
+    # of the all-gathered buffer (pos_c: chromosome c's start inside rank r's slice)
+    src = np.empty(total, dtype=np.int64)
     for r, s in enumerate(shards):
         pos = 0
         for c in s:
             n = int(windows_per_chrom[c])
-            track[offs[c]:offs[c] + n] = out[r * pad + pos: r * pad + pos + n]
+            src[offs[c]:offs[c] + n] = np.arange(r * pad + pos, r * pad + pos + n)
             pos += n
-    return track
+    return out.index_select(0, torch.from_numpy(src).to(out.device))
 
 
 def default_store():
