@@ -108,6 +108,17 @@ __global__ void __launch_bounds__(256) k_bounds(const gd_chrom_dev *ch, const in
   int32_t *lo = (pop ? lo_b : lo_a) + d.w_base;
   int32_t *hi = hi_a + d.w_base;
   const double inv = 1.0 / (double)wstep;
+  /* floor(a / wstep) for 0 <= a < 2^31 as a multiply-high (Granlund-Montgomery, N = 31:
+   * mag = ceil(2^(31+l) / wstep), l = ceil(log2 wstep)); other a (negative near the
+   * chromosome start, wstep == 1) take fdiv_fast */
+  int kl = 0;
+  while ((1ll << kl) < wstep) ++kl;
+  const uint32_t kmag = kl > 0 ? (uint32_t)(((1ull << (31 + kl)) + (uint64_t)wstep - 1) / (uint64_t)wstep) : 0u;
+  const uint32_t ksh = kl > 0 ? (uint32_t)(kl - 1) : 0u;
+  auto fl = [&](int64_t a) -> int64_t {
+    if (kl > 0 && a >= 0 && a < 0x80000000ll) return (int64_t)(__umulhi((uint32_t)a, kmag) >> ksh);
+    return fdiv_fast(a, wstep, inv);
+  };
   const bool aligned16 = ((pop ? d.b_off : d.a_off) & 3) == 0; /* int4 loads stay 16-byte aligned */
   /* each lane scans 16 consecutive elements (chromosome-relative i in [i0, i0+16)):
    * bit k of `bits` marks a boundary (i == 0, i == len, or pos[i] != pos[i-1]; three
@@ -123,22 +134,29 @@ __global__ void __launch_bounds__(256) k_bounds(const gd_chrom_dev *ch, const in
 #define KB_CH 4 /* int4 chunks per lane and segment (loads in flight) */
 #endif
   constexpr int KB_SEG = 256 * KB_CH;
+#ifndef KB_LDS
+#define KB_LDS 1
+#endif
+#if KB_LDS
+  __shared__ __attribute__((aligned(16))) int32_t kb_sh[4][KB_SEG];
+#endif
   const int lane = threadIdx.x & 63;
   const int64_t wave0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
   bool unsorted = false;
-  auto own = [&](int64_t i) { /* element i (a boundary: i == 0, i == len or pos[i] != pos[i-1]) */
+  /* element i (a boundary: i == 0, i == len or pos[i] != pos[i-1]) with p = pos[i] (i < len)
+   * and pp = pos[i-1] (i > 0) */
+  auto own = [&](int64_t i, int64_t p, int64_t pp) {
     const bool first = (i == 0), last = (i == len);
-    const int64_t p = last ? 0 : pos[i];
-    const int64_t pp = first ? 0 : pos[i - 1];
-    int64_t f = first ? 0 : fdiv_fast(pp, wstep, inv) + 1;
-    int64_t l = last ? wend - 1 : fdiv_fast(p, wstep, inv);
+    int64_t f = first ? 0 : fl(pp) + 1;
+    int64_t l = last ? wend - 1 : fl(p);
     if (f < 0) f = 0;
     if (l > wend - 1) l = wend - 1;
     for (int64_t w = f; w <= l; ++w) lo[w] = (int32_t)i;
     if (pop == 0) {
-      f = first ? 0 : -fdiv_fast(wsize - pp, wstep, inv);
-      l = last ? wend - 1 : -fdiv_fast(wsize - p, wstep, inv) - 1;
+      /* -floor((wsize - x) / wstep) = ceil((x - wsize) / wstep) = floor((x - wsize + wstep - 1) / wstep) */
+      f = first ? 0 : fl(pp - wsize + wstep - 1);
+      l = last ? wend - 1 : fl(p - wsize + wstep - 1) - 1;
       if (f < 0) f = 0;
       if (l > wend - 1) l = wend - 1;
       for (int64_t w = f; w <= l; ++w) hi[w] = (int32_t)i;
@@ -168,11 +186,30 @@ __global__ void __launch_bounds__(256) k_bounds(const gd_chrom_dev *ch, const in
       }
       if (seg == 0 && lane == 0) bits |= 1u; /* element 0 opens the first run */
       unsorted |= dec;
+#if KB_LDS
+      /* the segment in element order in the wave's LDS slice: the boundary walk reads
+       * pos[i] and pos[i - 1] from there instead of going back to memory */
+      int32_t *sg = kb_sh[threadIdx.x >> 6];
+#pragma unroll
+      for (int k = 0; k < KB_CH; ++k) *reinterpret_cast<int4 *>(sg + 256 * k + 4 * lane) = v[k];
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       while (bits) {
         const int b = __builtin_ctz(bits);
         bits &= bits - 1;
-        own(seg + 256 * (b >> 2) + 4 * lane + (b & 3));
+        const int r = 256 * (b >> 2) + 4 * lane + (b & 3);
+        own(seg + r, sg[r], r > 0 ? sg[r - 1] : before);
       }
+      __builtin_amdgcn_wave_barrier(); /* the slice is rewritten by the next segment */
+#else
+      while (bits) {
+        const int b = __builtin_ctz(bits);
+        bits &= bits - 1;
+        const int64_t i = seg + 256 * (b >> 2) + 4 * lane + (b & 3);
+        own(i, pos[i], i > 0 ? pos[i - 1] : 0);
+      }
+#endif
     } else {
       for (int64_t i0 = seg + 4 * KB_CH * lane; i0 < seg + KB_SEG && i0 <= len; i0 += KB_SEG) {
         int32_t prev = (i0 > 0) ? pos[i0 - 1] : 0;
@@ -181,7 +218,7 @@ __global__ void __launch_bounds__(256) k_bounds(const gd_chrom_dev *ch, const in
           const int32_t v = (i < len) ? pos[i] : 0;
           const bool bnd = (i == 0) || (i == len) || (v != prev);
           if (i > 0 && i < len) unsorted |= (v < prev);
-          if (bnd) own(i);
+          if (bnd) own(i, v, prev);
           prev = v;
         }
       }
