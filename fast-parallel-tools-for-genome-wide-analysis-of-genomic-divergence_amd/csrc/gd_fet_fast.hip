@@ -48,6 +48,9 @@
 #ifndef FW_SPAN
 #define FW_SPAN 1024 /* staged SNP rows per workgroup (32 windows need ~400 at 50 SNPs/window) */
 #endif
+#ifndef FW_STAGE_U
+#define FW_STAGE_U 4 /* 16-byte loads in flight per lane while staging the span */
+#endif
 #define FW_MAXREJ 8  /* rejected draws tracked per window before giving up */
 
 #define FW_BAD_GENERAL 1 /* hand the window to the literal general path */
@@ -318,12 +321,12 @@ __device__ void fw_stage_scores(const gd_chrom_dev &d, int r0, int nrows, const 
       atomicAdd(&cnt[__umulhi((uint32_t)relx, rmul)], ix);
       atomicAdd(&cnt[__umulhi((uint32_t)rely, rmul)], iy);
     };
-    for (int k0 = wave; k0 < nfull; k0 += 4 * NW) {
-      double2 v[4];
+    for (int k0 = wave; k0 < nfull; k0 += FW_STAGE_U * NW) {
+      double2 v[FW_STAGE_U];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) v[u] = v2[min(k0 + u * NW, nfull - 1) * 64 + lane];
+      for (int u = 0; u < FW_STAGE_U; ++u) v[u] = v2[min(k0 + u * NW, nfull - 1) * 64 + lane];
 #pragma unroll
-      for (int u = 0; u < 4; ++u)
+      for (int u = 0; u < FW_STAGE_U; ++u)
         if (k0 + u * NW < nfull) count_pair(v[u].x, v[u].y, k0 + u * NW, false);
     }
     if (nfull < nch && wave == NW - 1) { /* the partial last chunk, element by element */
