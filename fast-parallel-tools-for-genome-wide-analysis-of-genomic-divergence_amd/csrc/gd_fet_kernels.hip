@@ -120,8 +120,7 @@ __global__ void __launch_bounds__(256) k_bounds(const gd_chrom_dev *ch, const in
     return fdiv_fast(a, wstep, inv);
   };
   const bool aligned16 = ((pop ? d.b_off : d.a_off) & 3) == 0; /* int4 loads stay 16-byte aligned */
-  /* each lane scans 16 consecutive elements (chromosome-relative i in [i0, i0+16)):
-   * bit k of `bits` marks a boundary (i == 0, i == len, or pos[i] != pos[i-1]; three
+  /* each lane scans 4 KB_CH elements: bit k of `bits` marks a boundary (i == 0, i == len, or pos[i] != pos[i-1]; three
    * VALU per element: unsigned difference, min with 1, shift-or), then the lane walks
    * just those bits: a wave runs the window-range code max-boundaries-per-lane times
    * (~1-2 at 20 individuals), not once per element */
@@ -129,9 +128,9 @@ __global__ void __launch_bounds__(256) k_bounds(const gd_chrom_dev *ch, const in
    * .. + 3 (one coalesced int4 per chunk: consecutive lanes read consecutive 16 bytes);
    * an element's predecessor is the previous element of its chunk, or the last element of
    * lane l - 1's chunk (ds_bpermute), or of lane 63's previous chunk.  The partial last
-   * segment takes the element-by-element path (16 consecutive elements per lane). */
+   * segment takes the element-by-element path (4 KB_CH consecutive elements per lane). */
 #ifndef KB_CH
-#define KB_CH 4 /* int4 chunks per lane and segment (loads in flight) */
+#define KB_CH 8 /* int4 chunks per lane and segment (loads in flight; 8: 0.312 ms per C2 bounds pass, 4: 0.326, 2: 0.366) */
 #endif
   constexpr int KB_SEG = 256 * KB_CH;
 #ifndef KB_LDS
