@@ -130,7 +130,7 @@ __global__ void __launch_bounds__(256) k_bounds(const gd_chrom_dev *ch, const in
    * lane l - 1's chunk (ds_bpermute), or of lane 63's previous chunk.  The partial last
    * segment takes the element-by-element path (4 KB_CH consecutive elements per lane). */
 #ifndef KB_CH
-#define KB_CH 8 /* int4 chunks per lane and segment (loads in flight; 8: 0.312 ms per C2 bounds pass, 4: 0.326, 2: 0.366) */
+#define KB_CH 4 /* int4 chunks per lane and segment (loads in flight; 4: 0.326 ms per C2 bounds pass, 8: 0.312 (parity not yet run on the GPU), 2: 0.366) */
 #endif
   constexpr int KB_SEG = 256 * KB_CH;
 #ifndef KB_LDS
