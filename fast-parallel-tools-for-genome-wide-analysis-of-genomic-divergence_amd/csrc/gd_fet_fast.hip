@@ -42,7 +42,8 @@
 #define FW_WPB 32    /* windows per workgroup (sorted by (m, n) into waves of 8; 64 measured slower) */
 #endif
 #define FW_TPW 8     /* lanes per window (10 and 4 measured 35% / 22% slower) */
-#define FW_RPT 13    /* replicates per lane (8*13 >= 100; the last lane runs 9) */
+#define FW_RPT 12    /* whole replicates per lane: 8*12 = 96 */
+#define FW_HALF (FW_TPW / 2) /* replicates 96..99 drawn as halves by lane pairs (2j, 2j + 1) */
 #define FW_KTOP 24   /* ranked top scores kept per window (P(needing more) < 1e-9 per replicate) */
 #define FW_NFAST 256 /* largest window handled here */
 #ifndef FW_SPAN
@@ -155,93 +156,129 @@ __device__ __forceinline__ uint16_t rix_pack(int a, int b, int base) {
   return (uint16_t)(max(a - base, 0) | (max(b - base, 0) << 8));
 }
 
-/* lane's replicates [r0, r0 + nr) (nr <= FW_RPT): y already positioned at stream
- * position r0*n.  The draw loops run wave-uniform trip counts (scalar loop control):
- * nlo8 = 8 floor(min n / 8) draws unrolled by 8 for every lane, then draws up to the
- * wave's largest n with lanes past their own n masked off.  ymax collects the high
- * words; a draw was rejected iff (ymax >> 1) > limit.  muni: the wave's common m
- * (scalar), 0 when its windows differ. */
+/* Draws `len` values of one replicate (wave-uniform bounds lo8 <= len <= hi) into the
+ * top-MT list K */
 template <int MT>
-__device__ __forceinline__ void boot_lane(uint64_t y, int n, int nlo8, int nhi, uint64_t M, int nr, int m, int muni,
-                                          int base, uint16_t *rix, uint32_t &ymax, int &worst) {
-  uint32_t ylo = (uint32_t)y, yhi = (uint32_t)(y >> 32);
-  const uint32_t mlo = (uint32_t)M, mhi = (uint32_t)(M >> 32), D = 2u * (uint32_t)n;
-  for (int k = 0; k < FW_RPT; ++k) {
-    if (k < nr) {
-      uint32_t K[MT];
+__device__ __forceinline__ void draw_rep(uint32_t &ylo, uint32_t &yhi, uint32_t (&K)[MT], int len, int lo8, int hi,
+                                         uint32_t mlo, uint32_t mhi, uint32_t &ymax) {
 #pragma unroll
-      for (int i = 0; i < MT; ++i) K[i] = 0u;
-      int j = 0;
-      for (; j < nlo8; j += 8) {
-        FW_DRAW(MT);
-        FW_DRAW(MT);
-        FW_DRAW(MT);
-        FW_DRAW(MT);
-        FW_DRAW(MT);
-        FW_DRAW(MT);
-        FW_DRAW(MT);
-        FW_DRAW(MT);
+  for (int i = 0; i < MT; ++i) K[i] = 0u;
+  int j = 0;
+  for (; j < lo8; j += 8) {
+    FW_DRAW(MT);
+    FW_DRAW(MT);
+    FW_DRAW(MT);
+    FW_DRAW(MT);
+    FW_DRAW(MT);
+    FW_DRAW(MT);
+    FW_DRAW(MT);
+    FW_DRAW(MT);
+  }
+  for (; j < hi; ++j)
+    if (j < len) FW_DRAW(MT);
+}
+
+/* the rank pair of order statistics m-1, m-2 of a replicate's top list */
+template <int MT>
+__device__ __forceinline__ uint16_t pick_rix(const uint32_t (&K)[MT], int m, int muni, uint32_t D, int base,
+                                             int &worst) {
+  uint32_t ka = K[0], kb = K[0];
+  if (muni > 0) {
+    /* the wave shares one m (the usual case): static register picks */
+#pragma unroll
+    for (int i = 1; i < MT; ++i)
+      if (i == muni - 1) {
+        ka = K[i];
+        kb = K[i - 1];
       }
-      for (; j < nhi; ++j)
-        if (j < n) FW_DRAW(MT);
-      uint32_t ka = K[0], kb = K[0];
-      if (muni > 0) {
-        /* the wave shares one m (the usual case): static register picks */
+  } else {
 #pragma unroll
-        for (int i = 1; i < MT; ++i)
-          if (i == muni - 1) {
-            ka = K[i];
-            kb = K[i - 1];
-          }
-      } else {
-#pragma unroll
-        for (int i = 0; i < MT; ++i) {
-          if (i == m - 1) ka = K[i];
-          if (i == m - 2) kb = K[i];
-        }
-      }
-      const int a = fw_key_index(ka, D), b = fw_key_index(kb, D);
-      worst = min(worst, a); /* a = t_{m-1} <= b = t_{m-2}: the lowest index read */
-      rix[k] = rix_pack(a, b, base);
+    for (int i = 0; i < MT; ++i) {
+      if (i == m - 1) ka = K[i];
+      if (i == m - 2) kb = K[i];
     }
   }
+  const int a = fw_key_index(ka, D), b = fw_key_index(kb, D);
+  worst = min(worst, a); /* a = t_{m-1} <= b = t_{m-2}: the lowest index read */
+  return rix_pack(a, b, base);
+}
+
+/* Lane q's replicates: whole replicates 12q .. 12q + 11 from y (stream position 12qn),
+ * then half of replicate 96 + q/2 from yh (its first floor(n/2) draws for even q, the
+ * rest for odd q); the lane pair merges its two top lists (DPP quad_perm [1,0,3,2])
+ * and the even lane stores the replicate's rank pair.  8 lanes x 12.5 replicates: no
+ * idle replicate slot (13 per lane left 4 of 104 idle).  The draw loops run
+ * wave-uniform trip counts (scalar loop control): lo8 = 8 floor(min / 8) draws
+ * unrolled by 8 for every lane, then draws up to the wave's largest count with lanes
+ * past their own masked off.  ymax collects the high words; a draw was rejected iff
+ * (ymax >> 1) > limit.  muni: the wave's common m (scalar), 0 when its windows differ. */
+template <int MT>
+__device__ __forceinline__ void boot_lane(uint64_t y, uint64_t yh, int n, int nlo8, int nhi, int hlen, int hlo8,
+                                          int hhi, uint64_t M, int m, int muni, int base, uint16_t *rix,
+                                          uint16_t *rix_half, bool store_half, uint32_t &ymax, int &worst) {
+  const uint32_t mlo = (uint32_t)M, mhi = (uint32_t)(M >> 32), D = 2u * (uint32_t)n;
+  uint32_t ylo = (uint32_t)y, yhi = (uint32_t)(y >> 32);
+  for (int k = 0; k < FW_RPT; ++k) {
+    uint32_t K[MT];
+    draw_rep<MT>(ylo, yhi, K, n, nlo8, nhi, mlo, mhi, ymax);
+    rix[k] = pick_rix<MT>(K, m, muni, D, base, worst);
+  }
+  ylo = (uint32_t)yh;
+  yhi = (uint32_t)(yh >> 32);
+  uint32_t K[MT];
+  draw_rep<MT>(ylo, yhi, K, hlen, hlo8, hhi, mlo, mhi, ymax);
+  uint32_t P[MT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i) P[i] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)K[i], 0xB1, 0xF, 0xF, false);
+#pragma unroll
+  for (int i = 0; i < MT; ++i) top_insert_u<MT>(K, P[i]);
+  const uint16_t w = pick_rix<MT>(K, m, muni, D, base, worst);
+  if (store_half) *rix_half = w;
 }
 
 /* Per-n constants of the draw loop, built once per device (k_fet_ntab_build):
  * the rejection limit RAND_MAX - 2^31 mod n (cFisher.c:547-554), Lemire's
- * M = ceil(2^64 / 2n), and the nrand48 jump to stream position 13*q*n (lane q's
- * first replicate) as an affine map x -> mul*x + add (mod 2^48). */
+ * M = ceil(2^64 / 2n), and the nrand48 jumps to lane q's stream positions as affine
+ * maps x -> mul*x + add (mod 2^48): 12qn (its first whole replicate) and
+ * fw_half_start (its half replicate). */
 __device__ uint32_t g_ntab_limit[FW_NFAST + 1];
 __device__ uint64_t g_ntab_M[FW_NFAST + 1];
 __device__ uint64_t g_ntab_jmul[FW_NFAST + 1][FW_TPW];
 __device__ uint64_t g_ntab_jadd[FW_NFAST + 1][FW_TPW];
+__device__ uint64_t g_ntab_hmul[FW_NFAST + 1][FW_TPW];
+__device__ uint64_t g_ntab_hadd[FW_NFAST + 1][FW_TPW];
+
+/* stream position and length of lane q's half replicate (replicate 96 + q/2) */
+__device__ __forceinline__ int64_t fw_half_start(int q, int n) {
+  return (int64_t)(FW_TPW * FW_RPT + (q >> 1)) * n + ((q & 1) ? (n >> 1) : 0);
+}
+__device__ __forceinline__ int fw_half_len(int q, int n) { return (q & 1) ? n - (n >> 1) : (n >> 1); }
 
 /* Rare second pass for a window whose stream contains rejected draws
  * (random_int_nrand48 redraws while r > limit, cFisher.c:550-552): every draw
- * loops until accepted, starting from the lane's corrected stream position. */
-__device__ void boot_lane_rejecting(uint64_t y, int n, const gd_randint &rd, int nr, int m, int base,
-                                    uint16_t *rix, int &worst) {
-  for (int k = 0; k < nr; ++k) {
-    int K[8];
+ * loops until accepted, starting from the lane's corrected stream position.  One
+ * replicate's `len` draws into the index list K (top 8, descending). */
+__device__ void draw_rep_rejecting(uint64_t &y, int len, const gd_randint &rd, int (&K)[8]) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) K[i] = -1;
-    for (int j = 0; j < n; ++j) {
-      uint32_t hi;
-      do {
-        y = y * GD_LCG_A + FW_C16;
-        hi = (uint32_t)(y >> 32);
-      } while ((hi >> 1) > rd.limit);
-      top_insert<8>(K, fmod_n(hi >> 1, rd.magic, rd.shift, rd.n));
-    }
-    int a = K[0], b = K[0];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      if (i == m - 1) a = K[i];
-      if (i == m - 2) b = K[i];
-    }
-    worst = min(worst, a);
-    rix[k] = rix_pack(a, b, base);
+  for (int i = 0; i < 8; ++i) K[i] = -1;
+  for (int j = 0; j < len; ++j) {
+    uint32_t hi;
+    do {
+      y = y * GD_LCG_A + FW_C16;
+      hi = (uint32_t)(y >> 32);
+    } while ((hi >> 1) > rd.limit);
+    top_insert<8>(K, fmod_n(hi >> 1, rd.magic, rd.shift, rd.n));
   }
+}
+__device__ __forceinline__ uint16_t pick_rix_idx(const int (&K)[8], int m, int base, int &worst) {
+  int a = K[0], b = K[0];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    if (i == m - 1) a = K[i];
+    if (i == m - 2) b = K[i];
+  }
+  worst = min(worst, a);
+  return rix_pack(a, b, base);
 }
 
 __global__ void k_fet_ntab_build() {
@@ -254,6 +291,9 @@ __global__ void k_fet_ntab_build() {
     const gd_affine f = gd_lcg_jump((uint64_t)q * FW_RPT * nn);
     g_ntab_jmul[n][q] = f.mul;
     g_ntab_jadd[n][q] = f.add;
+    const gd_affine h = gd_lcg_jump((uint64_t)fw_half_start(q, (int)nn));
+    g_ntab_hmul[n][q] = h.mul;
+    g_ntab_hadd[n][q] = h.add;
   }
 }
 
@@ -342,6 +382,103 @@ __device__ void fw_stage_scores(const gd_chrom_dev &d, int r0, int nrows, const 
   }
 }
 
+/* Span staging by bit planes (the default wherever the planes fit in LDS).
+ *
+ * fetcount (cFisher.c:208-238) counts a row's "== 3" and "== -3" values.  Instead of
+ * per-value LDS atomics into per-row counters (fw_stage_scores: ~20 lanes of a wave add
+ * into one counter word, so every atomic is a ~10-way same-address conflict, and ~13
+ * VALU per value), every wave turns 64 consecutive values into two ballots (one
+ * v_cmp_eq_f64 each: 64 values per wave-instruction) that one lane stores.  The
+ * planes are the span's values in element order, population A then B: bit e of plane
+ * word w is value 64 w + e.  A row's counts are then four popcounts over its bit range
+ * (one lane per row, v_alignbit + v_bcnt), followed by the score-table lookup.
+ *
+ * Loads are raw buffer loads against the population's span (num_records = the span's
+ * bytes, so the partial last chunk reads zeros past the span, which compare false);
+ * per lane one VGPR offset, the 8 chunks of a group at immediate offsets 512 u.  A
+ * wave keeps 8 chunks of A and 8 of B in flight (32 VGPRs).
+ * Returns false (nothing written) when the planes exceed cap_words u64 words. */
+#ifndef FW_PL_U
+#define FW_PL_U 8 /* chunks per population in flight per wave */
+#endif
+__device__ __forceinline__ void *gd_uniform_ptr(const double *p) {
+  const uint64_t a = (uint64_t)(uintptr_t)p;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  return (void *)(uintptr_t)(((uint64_t)hi << 32) | lo);
+}
+/* popcount of plane bits [b, b + s): the planes are uint4 per 64-value chunk
+ * {"== 3" lo, hi, "== -3" lo, hi}; kind 0 / 2 selects the plane */
+__device__ __forceinline__ int fw_bits(const uint32_t *p32, int b, int s, int kind) {
+  int cnt = 0;
+  for (int o = 0; o < s; o += 32) {
+    const int e = b + o, w = min(s - o, 32);
+    const int i0 = ((e >> 6) << 2) + kind + ((e >> 5) & 1);
+    const int i1 = (e & 32) ? (((e >> 6) + 1) << 2) + kind : i0 + 1;
+    const uint32_t bits = __builtin_amdgcn_alignbit(p32[i1], p32[i0], (uint32_t)(e & 31));
+    cnt += __popc(w == 32 ? bits : (bits & ((1u << w) - 1u)));
+  }
+  return cnt;
+}
+
+__device__ bool fw_stage_planes(const gd_chrom_dev &d, int r0, int nrows, const double *avals, const double *bvals,
+                                const double *lut, uint4 *planes, int cap_chunks, double *dst) {
+  constexpr int NT = FW_WPB * FW_TPW, NW = NT / 64;
+  const int asize = d.asize, bsize = d.bsize;
+  const int nA = (nrows * asize + 63) >> 6, nB = (nrows * bsize + 63) >> 6, T = nA + nB;
+  if (T + 1 > cap_chunks) return false; /* workgroup-uniform */
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  /* the span bases are workgroup-uniform, but the compiler cannot prove it (the
+   * descriptor comes from a searched index): scalarise them, or every buffer load
+   * becomes a waterfall loop */
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
+      gd_uniform_ptr(avals + d.a_off + (int64_t)r0 * asize), (short)0,
+      __builtin_amdgcn_readfirstlane(nrows * asize * 8), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
+      gd_uniform_ptr(bvals + d.b_off + (int64_t)r0 * bsize), (short)0,
+      __builtin_amdgcn_readfirstlane(nrows * bsize * 8), 0x00020000);
+  /* wave w: chunks [a0, a1) of A and [b0, b1) of B */
+  const int ca = (nA + NW - 1) / NW, cbk = (nB + NW - 1) / NW;
+  const int a0 = min(wave * ca, nA), a1 = min(a0 + ca, nA), b0 = min(wave * cbk, nB), b1 = min(b0 + cbk, nB);
+  const int ngrp = max((a1 - a0 + FW_PL_U - 1) / FW_PL_U, (b1 - b0 + FW_PL_U - 1) / FW_PL_U);
+  for (int g = 0; g < ngrp; ++g) {
+    const int ka = a0 + g * FW_PL_U, kb = b0 + g * FW_PL_U;
+    const int va = (ka * 64 + lane) * 8, vb = (kb * 64 + lane) * 8;
+    /* unconditional loads: past this wave's range they read the next wave's values
+     * (ignored) or zeros past the span (num_records) */
+    double xa[FW_PL_U], xb[FW_PL_U];
+#pragma unroll
+    for (int u = 0; u < FW_PL_U; ++u) {
+      const auto v = __builtin_amdgcn_raw_buffer_load_b64(ra, va + 512 * u, 0, 0);
+      xa[u] = gd_f64_from(((uint64_t)v[1] << 32) | v[0]);
+      const auto w = __builtin_amdgcn_raw_buffer_load_b64(rb, vb + 512 * u, 0, 0);
+      xb[u] = gd_f64_from(((uint64_t)w[1] << 32) | w[0]);
+    }
+#pragma unroll
+    for (int u = 0; u < FW_PL_U; ++u) {
+      if (ka + u < a1) { /* wave-uniform */
+        const uint64_t m3 = __builtin_amdgcn_ballot_w64(xa[u] == 3.0), mm3 = __builtin_amdgcn_ballot_w64(xa[u] == -3.0);
+        if (lane == 0) planes[ka + u] = make_uint4((uint32_t)m3, (uint32_t)(m3 >> 32), (uint32_t)mm3, (uint32_t)(mm3 >> 32));
+      }
+      if (kb + u < b1) {
+        const uint64_t m3 = __builtin_amdgcn_ballot_w64(xb[u] == 3.0), mm3 = __builtin_amdgcn_ballot_w64(xb[u] == -3.0);
+        if (lane == 0)
+          planes[nA + kb + u] = make_uint4((uint32_t)m3, (uint32_t)(m3 >> 32), (uint32_t)mm3, (uint32_t)(mm3 >> 32));
+      }
+    }
+  }
+  if (threadIdx.x == 0) planes[T] = make_uint4(0, 0, 0, 0); /* read by the last rows' alignbit */
+  __syncthreads();
+  const int lut_nb = (bsize + 1) * (bsize + 2) / 2;
+  const uint32_t *p32 = reinterpret_cast<const uint32_t *>(planes);
+  for (int r = threadIdx.x; r < nrows; r += NT) {
+    const int ea = r * asize, eb = nA * 64 + r * bsize;
+    const int f0 = fw_bits(p32, ea, asize, 0), f1 = fw_bits(p32, ea, asize, 2);
+    const int f2 = fw_bits(p32, eb, bsize, 0), f3 = fw_bits(p32, eb, bsize, 2);
+    dst[r] = lut[(int64_t)gd_pair_index(f0, f1, asize) * lut_nb + gd_pair_index(f2, f3, bsize)];
+  }
+  return true;
+}
+
 /* one compare-exchange step of the lane-group bitonic sort: every register r meets
  * the partner lane's register (MIRROR ? 7 - r : r); the upper lane keeps the larger */
 template <int CTRL, bool MIRROR>
@@ -376,15 +513,16 @@ __global__ void __launch_bounds__(FW_WPB *FW_TPW)
   __shared__ double sh_span[FW_SPAN];
   /* the row counters of the span staging (fused mode) share LDS with the ranked top
    * scores and the replicate rank pairs, which are written only after it */
+  static_assert(FW_TPW * FW_RPT + FW_HALF == GD_NREP, "8 lanes x 12 whole + 4 halved replicates");
   __shared__ union {
     struct {
       double top[FW_WPB][FW_KTOP];
-      uint16_t rix[FW_WPB][FW_TPW * FW_RPT]; /* per replicate: rank pair read (rix_pack) */
+      uint16_t rix[FW_WPB][GD_NREP]; /* per replicate: rank pair read (rix_pack) */
     } b;
     uint32_t cnt[FW_SPAN]; /* per span row: majA | minA << 8 | majB << 16 | minB << 24 */
-  } sh_u;
+  } sh_u; /* fw_stage_planes also takes the whole union for its bit planes */
   double(&sh_top)[FW_WPB][FW_KTOP] = sh_u.b.top;
-  uint16_t(&sh_rix)[FW_WPB][FW_TPW * FW_RPT] = sh_u.b.rix;
+  uint16_t(&sh_rix)[FW_WPB][GD_NREP] = sh_u.b.rix;
   __shared__ int64_t sh_row[FW_WPB]; /* snp_score index of the window's first row; -1: not fast */
   __shared__ int sh_n[FW_WPB], sh_key[FW_WPB], sh_bad[FW_WPB], sh_slot[FW_WPB], sh_nrej[FW_WPB];
   __shared__ int sh_rej[FW_WPB][FW_MAXREJ];
@@ -468,7 +606,11 @@ __global__ void __launch_bounds__(FW_WPB *FW_TPW)
   if (spanlen > 0 && fused && gd_lut_holds(lut_hdr, d.asize, d.bsize, binom)) {
     /* fused: the span rows' -log10 p from the genotype values (fetcount + the score
      * table, as k_snp_fet) -- the values are read here, once per workgroup */
-    fw_stage_scores(d, (int)(span0 - d.a_off), spanlen, avals, bvals, lut, sh_u.cnt, sh_span);
+#ifndef GD_FET_ATOMIC_STAGE
+    if (!fw_stage_planes(d, (int)(span0 - d.a_off), spanlen, avals, bvals, lut, reinterpret_cast<uint4 *>(&sh_u),
+                         (int)(sizeof(sh_u) / sizeof(uint4)), sh_span))
+#endif
+      fw_stage_scores(d, (int)(span0 - d.a_off), spanlen, avals, bvals, lut, sh_u.cnt, sh_span);
   } else {
     /* k_snp_fet scored the rows (unfused mode, or sizes the table does not hold) */
     for (int i = tid; i < spanlen; i += FW_WPB * FW_TPW) sh_span[i] = snp_score[span0 + i];
@@ -554,65 +696,78 @@ __global__ void __launch_bounds__(FW_WPB *FW_TPW)
   __syncthreads();
 
   FW_PROF(1);
-  /* ---- B. bootstrap replicates: lane q runs replicates [13q, 13q+13) ---- */
+  /* ---- B. bootstrap replicates: lane q runs replicates [12q, 12q+12) and half of 96 + q/2 ---- */
   /* wave-uniform loop shape: the largest m (order statistics tracked) and the
-   * smallest / largest n among this wave's bootstrapped windows */
+   * smallest / largest n and half length among this wave's bootstrapped windows */
   const bool boot = fast && sh_bad[wl] == 0;
+  const int hlen = fw_half_len(q, n);
   int mmax = boot ? m : 0, mmin = boot ? m : 1 << 30, nmin = boot ? n : 1 << 30, nmax = boot ? n : 0;
+  int hmin = boot ? hlen : 1 << 30, hmax = boot ? hlen : 0;
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     mmax = max(mmax, __shfl_xor(mmax, o));
     mmin = min(mmin, __shfl_xor(mmin, o));
     nmin = min(nmin, __shfl_xor(nmin, o));
     nmax = max(nmax, __shfl_xor(nmax, o));
+    hmin = min(hmin, __shfl_xor(hmin, o));
+    hmax = max(hmax, __shfl_xor(hmax, o));
   }
   mmax = __builtin_amdgcn_readfirstlane(mmax);
   const int muni = __builtin_amdgcn_readfirstlane(mmin) == mmax ? mmax : 0;
   const int nlo8 = __builtin_amdgcn_readfirstlane(nmin) & ~7, nhi = __builtin_amdgcn_readfirstlane(nmax);
-  const int r0 = q * FW_RPT;
-  const int r1 = min(GD_NREP, r0 + FW_RPT);
+  const int hlo8 = __builtin_amdgcn_readfirstlane(hmin) & ~7, hhi = __builtin_amdgcn_readfirstlane(hmax);
+  const int r0 = q * FW_RPT, hrep = FW_TPW * FW_RPT + (q >> 1);
+  const bool hstore = (q & 1) == 0;
   const double delta = gd_perc_delta(n > 0 ? n : 1, perc, idx);
   const int nt = (n > 0 && n <= FW_NFAST) ? n : 1;
   const uint32_t limit = g_ntab_limit[nt];
   uint64_t x0 = 0;
   if (fast) x0 = gd_window_state(d.seed, GD_STREAM_FET, g - d.w_base);
-#ifdef GD_FET_NODRAW
-  const int nr = 0; /* diagnostics: setup cost only */
-#else
-  const int nr = r1 - r0;
-#endif
   uint16_t *rix = sh_rix[wl] + r0;
+#ifndef GD_FET_NODRAW /* diagnostics: setup cost only */
   if (boot) {
     const gd_affine jump = {g_ntab_jmul[nt][q], g_ntab_jadd[nt][q]};
-    const uint64_t x = gd_affine_apply(jump, x0), M = g_ntab_M[nt];
+    const gd_affine hjump = {g_ntab_hmul[nt][q], g_ntab_hadd[nt][q]};
+    const uint64_t x = gd_affine_apply(jump, x0), xh = gd_affine_apply(hjump, x0), M = g_ntab_M[nt];
     uint32_t ymax = 0;
     int worst = n;
     if (mmax <= 4)
-      boot_lane<4>(x << 16, n, nlo8, nhi, M, nr, m, muni, base, rix, ymax, worst);
+      boot_lane<4>(x << 16, xh << 16, n, nlo8, nhi, hlen, hlo8, hhi, M, m, muni, base, rix, sh_rix[wl] + hrep, hstore,
+                   ymax, worst);
     else if (mmax == 5)
-      boot_lane<5>(x << 16, n, nlo8, nhi, M, nr, m, muni, base, rix, ymax, worst);
+      boot_lane<5>(x << 16, xh << 16, n, nlo8, nhi, hlen, hlo8, hhi, M, m, muni, base, rix, sh_rix[wl] + hrep, hstore,
+                   ymax, worst);
     else
-      boot_lane<8>(x << 16, n, nlo8, nhi, M, nr, m, muni, base, rix, ymax, worst);
+      boot_lane<8>(x << 16, xh << 16, n, nlo8, nhi, hlen, hlo8, hhi, M, m, muni, base, rix, sh_rix[wl] + hrep, hstore,
+                   ymax, worst);
     if (worst < base) atomicOr(&sh_bad[wl], FW_BAD_GENERAL);
     if ((ymax >> 1) > limit) atomicOr(&sh_bad[wl], FW_BAD_REJECT);
   }
+#else
+  for (int k = 0; k < FW_RPT; ++k) rix[k] = 0;
+  if (hstore) sh_rix[wl][hrep] = 0;
+#endif
   __syncthreads();
 
   FW_PROF(2);
   /* ---- B'. windows whose stream rejected a draw (p ~ n*5000/2^31 per window):
-   * lane q locates the rejected positions of its pass-1 range [13qn, 13qn + len),
-   * the lanes then restart at the corrected positions P_q = 13qn + #(rejections
-   * before P_q) and redraw with the rejection loop.  Taken by ~1 in 300 workgroups. */
+   * lane q locates the rejected positions of its pass-1 ranges [12qn, 12qn + 12n) and
+   * its half replicate's, the lanes then restart each range at its corrected position
+   * P = start + #(rejections before P) and redraw with the rejection loop.  Taken by
+   * ~1 in 300 workgroups. */
   if (fast && sh_bad[wl] == FW_BAD_REJECT && q == 0) sh_nrej[wl] = 0;
   __syncthreads();
+  const int64_t hs = fw_half_start(q, n);
   if (fast && sh_bad[wl] == FW_BAD_REJECT) {
-    const int64_t p0 = (int64_t)r0 * n, len = (int64_t)(r1 - r0) * n;
-    uint64_t y = gd_affine_apply(gd_lcg_jump((uint64_t)p0), x0) << 16;
-    for (int64_t t = 0; t < len; ++t) {
-      y = y * GD_LCG_A + FW_C16;
-      if (((uint32_t)(y >> 32) >> 1) > limit) {
-        const int k = atomicAdd(&sh_nrej[wl], 1);
-        if (k < FW_MAXREJ) sh_rej[wl][k] = (int)(p0 + t);
+    for (int part = 0; part < 2; ++part) {
+      const int64_t p0 = part ? hs : (int64_t)r0 * n, len = part ? hlen : (int64_t)FW_RPT * n;
+      uint64_t y = gd_affine_apply(gd_lcg_jump((uint64_t)p0), x0) << 16;
+      for (int64_t t = 0; t < len; ++t) {
+        y = y * GD_LCG_A + FW_C16;
+        if (((uint32_t)(y >> 32) >> 1) > limit) {
+          const int k = atomicAdd(&sh_nrej[wl], 1);
+          if (k < FW_MAXREJ) sh_rej[wl][k] = (int)(p0 + t);
+        }
       }
     }
   }
@@ -622,19 +777,36 @@ __global__ void __launch_bounds__(FW_WPB *FW_TPW)
     if (nrej > FW_MAXREJ) {
       if (q == 0) sh_bad[wl] |= FW_BAD_GENERAL;
     } else {
-      /* fixed point: P = 13qn + #(rejected positions < P); all such positions lie in [0, 100n) */
-      int64_t c = 0;
-      for (;;) {
-        const int64_t P = (int64_t)r0 * n + c;
-        int64_t cnt = 0;
-        for (int k = 0; k < nrej; ++k) cnt += (sh_rej[wl][k] < P);
-        if (cnt == c) break;
-        c = cnt;
+      /* fixed points: P = start + #(rejected positions < P); all such positions lie in [0, 100n) */
+      int64_t P[2];
+      for (int part = 0; part < 2; ++part) {
+        const int64_t s0 = part ? hs : (int64_t)r0 * n;
+        int64_t c = 0;
+        for (;;) {
+          int64_t cnt = 0;
+          for (int k = 0; k < nrej; ++k) cnt += (sh_rej[wl][k] < s0 + c);
+          if (cnt == c) break;
+          c = cnt;
+        }
+        P[part] = s0 + c;
       }
-      const uint64_t y = gd_affine_apply(gd_lcg_jump((uint64_t)r0 * n + c), x0) << 16;
       int worst = n;
       const gd_randint rd = gd_randint_make((uint32_t)n);
-      boot_lane_rejecting(y, n, rd, nr, m, base, rix, worst);
+      uint64_t y = gd_affine_apply(gd_lcg_jump((uint64_t)P[0]), x0) << 16;
+      int K[8];
+      for (int k = 0; k < FW_RPT; ++k) {
+        draw_rep_rejecting(y, n, rd, K);
+        rix[k] = pick_rix_idx(K, m, base, worst);
+      }
+      y = gd_affine_apply(gd_lcg_jump((uint64_t)P[1]), x0) << 16;
+      draw_rep_rejecting(y, hlen, rd, K);
+      int Pk[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) Pk[i] = __builtin_amdgcn_update_dpp(0, K[i], 0xB1, 0xF, 0xF, false);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) top_insert<8>(K, Pk[i]);
+      const uint16_t w = pick_rix_idx(K, m, base, worst);
+      if (hstore) sh_rix[wl][hrep] = w;
       if (worst < base) atomicOr(&sh_bad[wl], FW_BAD_GENERAL);
     }
   }
@@ -642,30 +814,37 @@ __global__ void __launch_bounds__(FW_WPB *FW_TPW)
 
   FW_PROF(3);
   /* ---- C. window score + population std of the 100 replicates (std, cFisher.c:492-518):
-   * the sums run over i = 99 .. 0 exactly as the reference's loop, as one chain that
-   * walks down the window's 8 lanes (lane q holds replicates 13q ..), handed from
-   * lane to lane with a DPP row shift */
+   * the sums run over i = 99 .. 0 exactly as the reference's loop: replicates 99 .. 96
+   * (held by lanes 6, 4, 2, 0) gathered into lane 7, then one chain that walks down the
+   * window's 8 lanes (lane q holds replicates 12q .. 12q + 11), handed from lane to lane
+   * with a DPP row shift */
   const bool live = fast && !(sh_bad[wl] & FW_BAD_GENERAL);
-  double rep[FW_RPT]; /* this lane's replicates r0 .. r1-1, rebuilt from their rank pairs */
+  double rep[FW_RPT]; /* this lane's replicates r0 .. r0 + 11, rebuilt from their rank pairs */
 #pragma unroll
   for (int k = 0; k < FW_RPT; ++k) {
     rep[k] = 0.0;
-    if (live && k < nr) {
+    if (live) {
       const unsigned w = rix[k];
       rep[k] = gd_perc_mix(delta, sh_top[wl][w & 255u], sh_top[wl][w >> 8]);
     }
   }
-  double sum = 0.0;
+  double rh = 0.0; /* replicate 96 + q/2 (meaningful in even lanes) */
+  if (live && hstore) {
+    const unsigned w = sh_rix[wl][hrep];
+    rh = gd_perc_mix(delta, sh_top[wl][w & 255u], sh_top[wl][w >> 8]);
+  }
+  const int gl = (int)(threadIdx.x & ~7u); /* the window's lane 0 */
+  double h99 = __shfl(rh, gl + 6), h98 = __shfl(rh, gl + 4), h97 = __shfl(rh, gl + 2), h96 = __shfl(rh, gl);
+  double sum = (live && q == FW_TPW - 1) ? ((h99 + h98) + h97) + h96 : 0.0;
 #pragma unroll
   for (int step = FW_TPW - 1; step >= 0; --step) {
     if (live && q == step) {
 #pragma unroll
-      for (int k = FW_RPT - 1; k >= 0; --k)
-        if (k < nr) sum += rep[k];
+      for (int k = FW_RPT - 1; k >= 0; --k) sum += rep[k];
     }
     if (step > 0) sum = dpp_f64<0x101>(sum); /* row_shl:1: lane l takes lane l+1's partial */
   }
-  const double mu = __shfl(sum, (int)(threadIdx.x & ~7u)) / GD_NREP;
+  const double mu = __shfl(sum, gl) / GD_NREP;
   /* the squared deviations off the chain, all lanes at once (no FMA: the same two
    * roundings as the reference's (x - m) * (x - m)); the chain only adds */
 #pragma unroll
@@ -673,13 +852,19 @@ __global__ void __launch_bounds__(FW_WPB *FW_TPW)
     const double dd = rep[k] - mu;
     rep[k] = dd * dd;
   }
-  double ss = 0.0;
+  {
+    const double d99 = h99 - mu, d98 = h98 - mu, d97 = h97 - mu, d96 = h96 - mu;
+    h99 = d99 * d99;
+    h98 = d98 * d98;
+    h97 = d97 * d97;
+    h96 = d96 * d96;
+  }
+  double ss = (live && q == FW_TPW - 1) ? ((h99 + h98) + h97) + h96 : 0.0;
 #pragma unroll
   for (int step = FW_TPW - 1; step >= 0; --step) {
     if (live && q == step) {
 #pragma unroll
-      for (int k = FW_RPT - 1; k >= 0; --k)
-        if (k < nr) ss += rep[k];
+      for (int k = FW_RPT - 1; k >= 0; --k) ss += rep[k];
     }
     if (step > 0) ss = dpp_f64<0x101>(ss);
   }
