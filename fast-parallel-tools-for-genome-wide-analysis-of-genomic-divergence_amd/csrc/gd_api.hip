@@ -112,6 +112,8 @@ struct gd_ctx {
   size_t io_cap = 0;
   hipEvent_t ev[GD_NSTAGES + 1] = {};
   unsigned *h_flags = nullptr; /* pinned */
+  char *h_stage = nullptr;     /* pinned staging of the per-call descriptors (h2d) */
+  size_t h_stage_cap = 0, h_stage_off = 0;
   unsigned *h_flags_dev = nullptr; /* one device word (packer status) */
 };
 
@@ -187,6 +189,7 @@ extern "C" void gd_ctx_destroy(gd_ctx *c) {
   if (c->stream2) (void)hipStreamDestroy(c->stream2);
   if (c->stream_mem) (void)hipStreamDestroy(c->stream_mem);
   if (c->h_flags) (void)hipHostFree(c->h_flags);
+  if (c->h_stage) (void)hipHostFree(c->h_stage);
   if (c->h_flags_dev) (void)hipFree(c->h_flags_dev);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
@@ -348,6 +351,29 @@ static int make_plan_packed(const PackedIn &pk, int nchrom, int wsize, int wstep
   return GD_OK;
 }
 
+/* Host -> device copy of a per-call descriptor array through the context's pinned
+ * staging buffer, so the copy is a plain asynchronous DMA (a pageable source makes
+ * hipMemcpyAsync stage it synchronously).  Every scan call ends with a stream sync, so
+ * the buffer is free again at the next call (h_stage_off is reset there). */
+static int h2d(gd_ctx *c, void *dst, const void *src, size_t bytes, hipStream_t s) {
+  const size_t need = (c->h_stage_off + bytes + 255) & ~(size_t)255;
+  if (need > c->h_stage_cap) {
+    HIP_TRY(hipStreamSynchronize(s)); /* earlier staged copies of this call have landed */
+    if (c->h_stage) (void)hipHostFree(c->h_stage);
+    c->h_stage = nullptr;
+    c->h_stage_cap = 0;
+    c->h_stage_off = 0;
+    const size_t cap = std::max<size_t>(std::max<size_t>(need, 2 * bytes + 256), 1 << 16);
+    HIP_TRY(hipHostMalloc(&c->h_stage, cap));
+    c->h_stage_cap = cap;
+  }
+  char *p = c->h_stage + c->h_stage_off;
+  std::memcpy(p, src, bytes);
+  c->h_stage_off = (c->h_stage_off + bytes + 255) & ~(size_t)255;
+  HIP_TRY(hipMemcpyAsync(dst, p, bytes, hipMemcpyHostToDevice, s));
+  return GD_OK;
+}
+
 static int flags_to_status(unsigned f) {
   if (f & (GD_FLAG_UNSORTED_A | GD_FLAG_UNSORTED_B)) return fail(GD_ERR_UNSORTED, "positions are not sorted");
   if (f & GD_FLAG_B_BOUNDS) return fail(GD_ERR_BOUNDS, "a window's B slice runs past blen");
@@ -410,13 +436,13 @@ static int fet_scan_locked(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, cons
   Carve real{ctx->ws};
   layout_all(real);
   unsigned *list_count = flags + 4, *huge_count = flags + 8;
+  ctx->h_stage_off = 0;
   if (pk) {
-    HIP_TRY(hipMemcpyAsync(d_roff, row_off.data(), sizeof(int64_t) * nchrom, hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemcpyAsync(d_woff, word_off.data(), sizeof(int64_t) * 2 * nchrom, hipMemcpyHostToDevice, s));
+    if ((st = h2d(ctx, d_roff, row_off.data(), sizeof(int64_t) * nchrom, s))) return st;
+    if ((st = h2d(ctx, d_woff, word_off.data(), sizeof(int64_t) * 2 * nchrom, s))) return st;
   }
-
-  HIP_TRY(hipMemcpyAsync(d_ch, pl.h.data(), sizeof(gd_chrom_dev) * nchrom, hipMemcpyHostToDevice, s));
-  HIP_TRY(hipMemcpyAsync(d_blk, blk_off.data(), sizeof(int32_t) * (nchrom + 1), hipMemcpyHostToDevice, s));
+  if ((st = h2d(ctx, d_ch, pl.h.data(), sizeof(gd_chrom_dev) * nchrom, s))) return st;
+  if ((st = h2d(ctx, d_blk, blk_off.data(), sizeof(int32_t) * (nchrom + 1), s))) return st;
   HIP_TRY(hipMemsetAsync(flags, 0, 16 * sizeof(unsigned), s));
   HIP_TRY(hipEventRecord(ctx->ev[0], s));
   /* Pipeline over chromosome groups on the context's two streams: the HBM-bound

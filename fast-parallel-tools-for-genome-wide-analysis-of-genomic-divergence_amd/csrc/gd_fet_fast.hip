@@ -307,6 +307,29 @@ __device__ __forceinline__ double dpp_f64(double v) {
   const int hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(u >> 32), CTRL, 0xF, 0xF, false);
   return gd_f64_from(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
 }
+/* the same exchange for patterns whose every lane has a source (quad_perm,
+ * row_half_mirror): bound_ctrl DPP movs, so no "old" value is materialised or copied
+ * per exchange */
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64_full(double v) {
+  const uint64_t u = gd_f64_bits(v);
+  const int lo = __builtin_amdgcn_mov_dpp((int)(uint32_t)u, CTRL, 0xF, 0xF, true);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(uint32_t)(u >> 32), CTRL, 0xF, 0xF, true);
+  return gd_f64_from(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+/* v_max_f64 / v_min_f64 without the canonicalisation fmax/fmin add in front of every
+ * operand: a window with a NaN score is handed to the general path anyway */
+__device__ __forceinline__ double fw_max(double a, double b) {
+  double r;
+  asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ double fw_min(double a, double b) {
+  double r;
+  asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+
 __device__ __forceinline__ double group8_max(double v) {
   v = fmax(v, dpp_f64<0xB1>(v));  /* quad_perm [1,0,3,2] */
   v = fmax(v, dpp_f64<0x4E>(v));  /* quad_perm [2,3,0,1] */
@@ -485,7 +508,7 @@ template <int CTRL, bool MIRROR>
 __device__ __forceinline__ void fw_cross(double (&v)[8], bool upper) {
   double p[8];
 #pragma unroll
-  for (int r = 0; r < 8; ++r) p[r] = dpp_f64<CTRL>(v[MIRROR ? 7 - r : r]);
+  for (int r = 0; r < 8; ++r) p[r] = dpp_f64_full<CTRL>(v[MIRROR ? 7 - r : r]);
 #pragma unroll
   for (int r = 0; r < 8; ++r) v[r] = ((v[r] > p[r]) == upper) ? v[r] : p[r];
 }
@@ -494,8 +517,8 @@ __device__ __forceinline__ void fw_cross(double (&v)[8], bool upper) {
 __device__ __forceinline__ void fw_clean8(double (&v)[8]) {
 #define FW_CX2(a, b)                       \
   do {                                     \
-    const double hi_ = fmax(v[a], v[b]);   \
-    v[b] = fmin(v[a], v[b]);               \
+    const double hi_ = fw_max(v[a], v[b]); \
+    v[b] = fw_min(v[a], v[b]);             \
     v[a] = hi_;                            \
   } while (0)
   FW_CX2(0, 4); FW_CX2(1, 5); FW_CX2(2, 6); FW_CX2(3, 7);
@@ -650,8 +673,8 @@ __global__ void __launch_bounds__(FW_WPB *FW_TPW)
       /* Batcher odd-even merge sort network for 8 keys, descending */
 #define FW_CX(a, b)                         \
   do {                                      \
-    const double hi_ = fmax(v[a], v[b]);    \
-    v[b] = fmin(v[a], v[b]);                \
+    const double hi_ = fw_max(v[a], v[b]);  \
+    v[b] = fw_min(v[a], v[b]);              \
     v[a] = hi_;                             \
   } while (0)
       FW_CX(0, 1); FW_CX(2, 3); FW_CX(4, 5); FW_CX(6, 7);

@@ -7,6 +7,7 @@
 #   smoke                __graft_entry__.smoke()
 #   bench[=ARGS]         python bench.py ARGS (underscores in ARGS become spaces)
 #   fet[=TAG]            FET-only bench (20 steps), libgdscan.so of tools/ab/TAG if given
+#   fetenv=K=V,...       FET-only bench with environment variables set (e.g. GD_GROUPS=2)
 #   valu[=TAG]           SQ VALU/LDS counters of the FET-only bench, variant TAG if given
 #   css[=ENV]            tools/css_time.py with ENV (e.g. POP=40,NCH=4,RUNS=0,STEPS=5)
 # Variants are built on the CPU beforehand: tools/build_variant.sh TAG "-DFLAG ..."
@@ -32,6 +33,9 @@ for S in "$@"; do
     fet)
       L=$(lib "$V"); env ${L:+GDSCAN_LIB=$L} timeout -k 10 120 python3 bench.py --steps 20 --warmup 3 --no-css --no-extra \
         --no-cpu > $O/$i.fet$V.json 2> $O/$i.fet$V.err ;;
+    fetenv)
+      env ${V//,/ } timeout -k 10 120 python3 bench.py --steps 20 --warmup 3 --no-css --no-extra \
+        --no-cpu > $O/$i.fetenv.json 2> $O/$i.fetenv.err ;;
     valu)
       L=$(lib "$V"); env ${L:+GDSCAN_LIB=$L} timeout -s KILL 150 rocprofv3 --pmc $SQ -d $O/$i.valu$V -o run \
         --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu --no-css --no-extra \
