@@ -178,19 +178,21 @@ __device__ __forceinline__ void draw_rep(uint32_t &ylo, uint32_t &yhi, uint32_t 
     if (j < len) FW_DRAW(MT);
 }
 
-/* the rank pair of order statistics m-1, m-2 of a replicate's top list */
-template <int MT>
-__device__ __forceinline__ uint16_t pick_rix(const uint32_t (&K)[MT], int m, int muni, uint32_t D, int base,
-                                             int &worst) {
+/* The rank pair of order statistics m-1, m-2 of a replicate's top list, packed as
+ * rix_pack does, in four VALU: the index recovery (key + 1) D >> 33 and the
+ * subtraction of base are one v_mad_u64_u32 each, scaled by 2^7 so that rank - base
+ * lands in byte 1 of the high word (D 2^7 = 256 n < 2^17, (key + 1) D 2^7 < 2^49), and
+ * one v_perm_b32 joins the two bytes.  A rank below base leaves a wrapped byte, but
+ * its window goes to the general path: wkey keeps the smallest key read (keys grow
+ * with the index), checked once per lane.  MU > 0: the wave's common m, the register
+ * picks are static; MU = 0: per-lane m. */
+template <int MT, int MU>
+__device__ __forceinline__ uint16_t pick_rix(const uint32_t (&K)[MT], int m, uint32_t D7, uint64_t add7,
+                                             uint32_t &wkey) {
   uint32_t ka = K[0], kb = K[0];
-  if (muni > 0) {
-    /* the wave shares one m (the usual case): static register picks */
-#pragma unroll
-    for (int i = 1; i < MT; ++i)
-      if (i == muni - 1) {
-        ka = K[i];
-        kb = K[i - 1];
-      }
+  if (MU > 0) {
+    ka = K[MU - 1];
+    kb = K[MU >= 2 ? MU - 2 : 0];
   } else {
 #pragma unroll
     for (int i = 0; i < MT; ++i) {
@@ -198,9 +200,9 @@ __device__ __forceinline__ uint16_t pick_rix(const uint32_t (&K)[MT], int m, int
       if (i == m - 2) kb = K[i];
     }
   }
-  const int a = fw_key_index(ka, D), b = fw_key_index(kb, D);
-  worst = min(worst, a); /* a = t_{m-1} <= b = t_{m-2}: the lowest index read */
-  return rix_pack(a, b, base);
+  wkey = min(wkey, ka); /* a = t_{m-1} <= b = t_{m-2}: the lowest index read */
+  const uint32_t ha = (uint32_t)(((uint64_t)ka * D7 + add7) >> 32), hb = (uint32_t)(((uint64_t)kb * D7 + add7) >> 32);
+  return (uint16_t)__builtin_amdgcn_perm(hb, ha, 0x0C0C0501u);
 }
 
 /* Lane q's replicates: whole replicates 12q .. 12q + 11 from y (stream position 12qn),
@@ -212,16 +214,18 @@ __device__ __forceinline__ uint16_t pick_rix(const uint32_t (&K)[MT], int m, int
  * unrolled by 8 for every lane, then draws up to the wave's largest count with lanes
  * past their own masked off.  ymax collects the high words; a draw was rejected iff
  * (ymax >> 1) > limit.  muni: the wave's common m (scalar), 0 when its windows differ. */
-template <int MT>
+template <int MT, int MU>
 __device__ __forceinline__ void boot_lane(uint64_t y, uint64_t yh, int n, int nlo8, int nhi, int hlen, int hlo8,
-                                          int hhi, uint64_t M, int m, int muni, int base, uint16_t *rix,
-                                          uint16_t *rix_half, bool store_half, uint32_t &ymax, int &worst) {
-  const uint32_t mlo = (uint32_t)M, mhi = (uint32_t)(M >> 32), D = 2u * (uint32_t)n;
+                                          int hhi, uint64_t M, int m, int base, uint16_t *rix, uint16_t *rix_half,
+                                          bool store_half, uint32_t &ymax, uint32_t &wkey) {
+  const uint32_t mlo = (uint32_t)M, mhi = (uint32_t)(M >> 32), D7 = 256u * (uint32_t)n;
+  const uint64_t add7 = (uint64_t)D7 - ((uint64_t)base << 40);
   uint32_t ylo = (uint32_t)y, yhi = (uint32_t)(y >> 32);
+#pragma unroll 2
   for (int k = 0; k < FW_RPT; ++k) {
     uint32_t K[MT];
     draw_rep<MT>(ylo, yhi, K, n, nlo8, nhi, mlo, mhi, ymax);
-    rix[k] = pick_rix<MT>(K, m, muni, D, base, worst);
+    rix[k] = pick_rix<MT, MU>(K, m, D7, add7, wkey);
   }
   ylo = (uint32_t)yh;
   yhi = (uint32_t)(yh >> 32);
@@ -232,7 +236,7 @@ __device__ __forceinline__ void boot_lane(uint64_t y, uint64_t yh, int n, int nl
   for (int i = 0; i < MT; ++i) P[i] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)K[i], 0xB1, 0xF, 0xF, false);
 #pragma unroll
   for (int i = 0; i < MT; ++i) top_insert_u<MT>(K, P[i]);
-  const uint16_t w = pick_rix<MT>(K, m, muni, D, base, worst);
+  const uint16_t w = pick_rix<MT, MU>(K, m, D7, add7, wkey);
   if (store_half) *rix_half = w;
 }
 
@@ -752,18 +756,27 @@ __global__ void __launch_bounds__(FW_WPB *FW_TPW)
     const gd_affine jump = {g_ntab_jmul[nt][q], g_ntab_jadd[nt][q]};
     const gd_affine hjump = {g_ntab_hmul[nt][q], g_ntab_hadd[nt][q]};
     const uint64_t x = gd_affine_apply(jump, x0), xh = gd_affine_apply(hjump, x0), M = g_ntab_M[nt];
-    uint32_t ymax = 0;
-    int worst = n;
-    if (mmax <= 4)
-      boot_lane<4>(x << 16, xh << 16, n, nlo8, nhi, hlen, hlo8, hhi, M, m, muni, base, rix, sh_rix[wl] + hrep, hstore,
-                   ymax, worst);
-    else if (mmax == 5)
-      boot_lane<5>(x << 16, xh << 16, n, nlo8, nhi, hlen, hlo8, hhi, M, m, muni, base, rix, sh_rix[wl] + hrep, hstore,
-                   ymax, worst);
-    else
-      boot_lane<8>(x << 16, xh << 16, n, nlo8, nhi, hlen, hlo8, hhi, M, m, muni, base, rix, sh_rix[wl] + hrep, hstore,
-                   ymax, worst);
-    if (worst < base) atomicOr(&sh_bad[wl], FW_BAD_GENERAL);
+    uint32_t ymax = 0, wkey = ~0u;
+#define FW_BOOT(MT, MU)                                                                                          \
+  boot_lane<MT, MU>(x << 16, xh << 16, n, nlo8, nhi, hlen, hlo8, hhi, M, m, base, rix, sh_rix[wl] + hrep, hstore, \
+                    ymax, wkey)
+    if (mmax <= 4) {
+      if (muni == 4)
+        FW_BOOT(4, 4);
+      else if (muni == 3)
+        FW_BOOT(4, 3);
+      else
+        FW_BOOT(4, 0);
+    } else if (mmax == 5) {
+      if (muni == 5)
+        FW_BOOT(5, 5);
+      else
+        FW_BOOT(5, 0);
+    } else {
+      FW_BOOT(8, 0);
+    }
+#undef FW_BOOT
+    if (fw_key_index(wkey, 2u * (uint32_t)n) < base) atomicOr(&sh_bad[wl], FW_BAD_GENERAL);
     if ((ymax >> 1) > limit) atomicOr(&sh_bad[wl], FW_BAD_REJECT);
   }
 #else
