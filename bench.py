@@ -51,23 +51,15 @@ sys.path.insert(0, str(PKG))
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, HBM3E spec
 FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 vector spec
-PROFILE_ROUND = "r03"
+MFMA_I8_PEAK_TOPS = 5000.0  # MI355X_MICROARCH.md: I8 MFMA at 2x the BF16 rate (~2.5 PF dense)
+VALU_ISSUE_GINSTS = 256 * 4 * 2.4 / 4  # one wave64 VALU instruction per SIMD per 4 cycles (SIMD16)
+PROFILE_ROUND = "r04"
 PROF = ROOT / "profiles"
 TRAFFIC_FILE = PROF / f"{PROFILE_ROUND}_fet_traffic.json"
 VALU_FILE = PROF / f"{PROFILE_ROUND}_fet_valu.json"
 CSS_VALU_FILE = PROF / f"{PROFILE_ROUND}_css_valu.json"
 UBENCH_FILE = PROF / f"{PROFILE_ROUND}_ubench_valu.json"
-
-
-def valu_peak():
-    """VALU issue peak in G wave-instructions/s: the measured simple-integer/FP32 issue rate
-    of tools/ubench_valu.hip (profiles/<R>_ubench_valu.json) when committed, else the
-    MI355X_MICROARCH.md figure (a wave64 instruction over 2 cycles on a SIMD-32 once two or
-    more waves share it: 256 CUs x 4 SIMDs x 2.4 GHz / 2)."""
-    if UBENCH_FILE.exists():
-        u = json.loads(UBENCH_FILE.read_text())
-        return float(u["peak_ginsts"]), f"{UBENCH_FILE.relative_to(ROOT)} ({u['method']})"
-    return 256 * 4 * 2.4 / 2, "MI355X_MICROARCH.md (2 cycles per wave64 VALU instruction per SIMD)"
+CSS_PHASE_FILE = PROF / f"{PROFILE_ROUND}_css_phases.json"
 
 
 def parse():
@@ -87,12 +79,14 @@ def parse():
     ap.add_argument("--no-css", action="store_true", help="skip the CSS legs")
     ap.add_argument("--no-c45", action="store_true", help="skip the C4/C5 CSS legs")
     ap.add_argument("--no-extra", action="store_true", help="skip the region-filter and packed-track legs")
-    ap.add_argument("--css-steps", type=int, default=3)
+    ap.add_argument("--css-steps", type=int, default=5, help="C3 timed steps (median reported)")
     ap.add_argument("--c45-chroms", type=int, default=25, help="C4/C5 chromosomes per GPU (configs[3]/[4]: 200/8)")
-    ap.add_argument("--c45-steps", type=int, default=2)
+    ap.add_argument("--c45-steps", type=int, default=5, help="C4/C5 timed steps (median reported)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target wall time of each CSS CPU sample")
     ap.add_argument("--backend", default="nccl")
     ap.add_argument("--dry-run", action="store_true", help="distributed plumbing only, no GPU work (CPU tests)")
+    ap.add_argument("--force-dist", action="store_true",
+                    help="initialise torch.distributed even at one rank (exercises the RCCL gathers on one GPU)")
     return ap.parse_args()
 
 
@@ -198,14 +192,14 @@ def fet_cpu_baseline(args, scores_dev, chroms):
     threads = 64 if kind == "reference" else 1
     return {
         "value": total_w / total_t, "unit": "windows/s", "cores": min(threads, usable), "kind": kind,
-        "threads": threads, "nproc": nproc, "cpu_model": model,
-        "sample": f"{args.cpu_chroms} of the {args.nchrom} chromosomes ({args.nsnp} SNPs, {args.asize}+{args.bsize}), "
-                  f"{total_w} windows in {total_t:.2f} s"
-                  + (f" with the reference's 64 pthreads on {min(64, usable)} usable cores" if kind == "reference"
-                     else ", 1 thread"),
-        "parity": {"windows": nwin, "bit_exact_frac": exact / max(nwin, 1), "max_rel": max_rel,
-                   "what": "reference threadcompute scores vs the GPU scores of the same windows (scores are "
-                           "seed-independent; stddev is time-seeded in the reference)"},
+        "parity_windows": nwin, "parity_bit_exact_frac": exact / max(nwin, 1), "parity_max_rel": max_rel,
+        "threads": threads, "cpu_model": model,
+        "sample": f"{args.cpu_chroms}/{args.nchrom} chromosomes, {total_w} windows in {total_t:.2f} s"
+                  + (f", reference threadcompute, 64 pthreads on {min(64, usable)} cores" if kind == "reference"
+                     else ", oracle, 1 thread"),
+        "what": f"{kind} {'threadcompute (oracle/_ref, built from the reference sources)' if kind == 'reference' else 'orc_fet_scan'}"
+                "; parity = its scores vs the GPU scores of the same windows (seed-independent; the reference's "
+                "stddev is time-seeded)",
     }
 
 
@@ -248,11 +242,8 @@ def css_cpu_baseline(args, pop, treshold, runs):
         res = list(ex.map(lambda c: run(c, inputs[c]), range(threads)))
     wall = time.perf_counter() - t0
     win = sum(r[1] for r in res)
-    return {"value": win / wall, "unit": "windows/s", "cores": threads, "kind": "port", "nproc": nproc,
-            "cpu_model": model,
-            "sample": f"{threads} chromosome prefixes of {nsnp} SNPs ({pop}+{pop}, mcT={treshold}, mcR={runs}), one "
-                      f"per thread, {win} windows in {wall:.2f} s (oracle/css_oracle.c, cyclic-Jacobi restatement; "
-                      f"the reference CSS needs GSL, absent here)"}
+    return {"value": win / wall, "unit": "windows/s", "cores": threads, "kind": "port",
+            "sample": f"{threads} x {nsnp}-SNP prefixes, {win} windows in {wall:.2f} s"}
 
 
 # ----------------------------------------------------------------------------- FET extras
@@ -283,8 +274,7 @@ def regions_run(args, scores, stddev, chroms, nch, rank, world, dev):
     for _ in range(reps):
         lim, (first, end, ns) = run()
     ms = (time.perf_counter() - t0) * 1e3 / reps
-    res = {"what": "FilterFisherScores (limit + merge) on the device-resident FET track, 1 call",
-           "windows": int(sc.numel()), "ms": ms, "windows_per_s": sc.numel() / (ms * 1e-3),
+    res = {"windows": int(sc.numel()), "ms": ms, "windows_per_s": sc.numel() / (ms * 1e-3),
            "limit": lim[0], "selected": ns, "regions": int(len(first))}
     if rank == 0 and world == 1 and not args.no_cpu:
         sys.path.insert(0, str(ROOT / "oracle"))
@@ -298,8 +288,7 @@ def regions_run(args, scores, stddev, chroms, nch, rank, world, dev):
                                 lambda s: chroms[int(s)].regend - 1)
         cpu_ms = (time.perf_counter() - c0) * 1e3
         res["cpu_baseline"] = {"value": sc.numel() / (cpu_ms * 1e-3), "unit": "windows/s", "cores": 1,
-                               "kind": "port", "sample": f"the whole track ({sc.numel()} windows), numpy + "
-                               "Python loop restatement (oracle/regions_oracle.py)"}
+                               "kind": "port", "sample": "whole track, oracle/regions_oracle.py"}
         res["parity"] = bool(want[0] == lim[0] and [(int(f), int(e)) for f, e in zip(first, end)] == regs)
     return res
 
@@ -349,8 +338,7 @@ def packed_run(args, lib, _lib, check, ctx, stream, dev, avals, bvals, apos, bpo
                   for c in range(nch))
     ref_bytes = 12 * nch * nsnp * (a + b)
     packed_bytes = 8 * nch * nsnp * (wa + wb) + 4 * nch * nsnp
-    return {"what": "FET scan from packed genotype tracks (2-bit codes, one position per row), device-resident",
-            "ms_per_step": ms, "windows_per_s": windows / (ms * 1e-3), "steps": n, "pack_ms": pack_ms,
+    return {"ms_per_step": ms, "windows_per_s": windows / (ms * 1e-3), "steps": n, "pack_ms": pack_ms,
             "input_bytes": packed_bytes, "reference_layout_bytes": ref_bytes,
             "parity": bool(torch.equal(ps, scores) and torch.equal(pd, stddev))}, (ac, bc, rp, pcs)
 
@@ -403,8 +391,7 @@ def host_run(args, lib, _lib, check, avals, bvals, apos, bpos, chroms, nch, scor
         _lib.GD_WINDOWS_THREADED, pd_(s_), pd_(d_))))
     ref_bytes = 12 * (na + nb) + 16 * nw
     pk_bytes = 8 * nh * nsnp * (wa + wb) + 4 * nh * nsnp + 16 * nw
-    return {"what": "FET scan called with host buffers (PCIe transfers inside the call), best of 3",
-            "sample": f"{nh} chromosomes x {nsnp} SNPs ({a}+{b}), {windows} windows",
+    return {"sample": f"{nh} x {nsnp} SNPs, {windows} windows, host buffers, best of 3",
             "reference_layout": {"ms": t_ref * 1e3, "windows_per_s": windows / t_ref,
                                  "host_bytes": ref_bytes, "GB_per_s": ref_bytes / t_ref / 1e9},
             "packed": {"ms": t_pk * 1e3, "windows_per_s": windows / t_pk,
@@ -445,18 +432,38 @@ class Env:
 
 
 def css_valu(shape_key, windows, kernel_ms):
-    """VALU-issue figure of a CSS leg from the committed PMC profile (wave-instructions per
-    window of the kernels the leg dispatches), over this run's kernel time."""
+    """VALU figures of a CSS leg from the committed PMC profile: wave-instructions per
+    window of the kernels the leg dispatches over this run's kernel time (G/s), and the
+    SIMDs' VALU busy fraction of the dominant kernel as the counters saw it."""
     if not CSS_VALU_FILE.exists():
-        return None
+        return {}
     doc = json.loads(CSS_VALU_FILE.read_text()).get(shape_key)
     if not doc or kernel_ms <= 0:
-        return None
-    peak, src = valu_peak()
+        return {}
     gi = doc["valu_wave_insts_per_window"] * windows / (kernel_ms * 1e-3) / 1e9
-    return {"bound": "valu-issue", "achieved": gi, "peak": peak, "unit": "G wave-insts/s", "frac": gi / peak,
-            "insts_per_window": doc["valu_wave_insts_per_window"], "kernels": doc["kernels"],
-            "source": f"{CSS_VALU_FILE.relative_to(ROOT)} [{shape_key}] ({doc['method']}); peak: {src}"}
+    out = {"valu_ginsts": gi, "valu_insts_per_window": doc["valu_wave_insts_per_window"]}
+    if "valu_busy" in doc:
+        out["valu_busy"] = doc["valu_busy"]
+    return out
+
+
+def dist_build(shape_key, m, kernel_ms, windows):
+    """SURVEY.md 8(d)'s CSS distance-build figure: 4 m^2 npos integer ops per window
+    (compare_all, css.c:277-327) over the time the bit planes (k_css_pack) plus the
+    popcount distance build take -- the build's share of the MDS kernel from the
+    committed GD_CSS_PROFILE phase profile, k_css_pack's share of the stage from the
+    kernel trace -- against the MFMA int8 dense peak it would have used."""
+    if not CSS_PHASE_FILE.exists():
+        return None
+    doc = json.loads(CSS_PHASE_FILE.read_text()).get(shape_key)
+    if not doc or kernel_ms <= 0:
+        return None
+    share = doc["pack_share"] + (1.0 - doc["pack_share"]) * doc["d_share"]
+    ms = kernel_ms * share
+    ops = 4.0 * m * m * doc["npos_mean"]
+    return {"ops_per_window": ops, "share_of_window_time": share, "ms": ms,
+            "tops": ops * windows / (ms * 1e-3) / 1e12 if ms > 0 else None, "mfma_int8_peak_tops": MFMA_I8_PEAK_TOPS,
+            "pack_share": doc["pack_share"], "d_share_of_mds": doc["d_share"]}
 
 
 def perm_stats(pm, computed, treshold, runs, perm_ms, pop):
@@ -466,55 +473,54 @@ def perm_stats(pm, computed, treshold, runs, perm_ms, pop):
     early = p * (runs + 1) > treshold + 0.5
     nrun = np.where(early, np.rint((treshold + 1) / p) - 1, runs)
     perms = float(nrun.sum())
-    # (a*b + a + b) FP64 adds per permutation actually run
-    ach = perms * (pop * pop + 2 * pop) / (perm_ms * 1e-3) / 1e12 if perm_ms > 0 else 0.0
     return {"total": perms, "mean_per_window": float(nrun.mean()),
-            "histogram": {"<=10": int((nrun <= 10).sum()), "11-100": int(((nrun > 10) & (nrun <= 100)).sum()),
-                          f"101-{runs - 1}": int(((nrun > 100) & (nrun < runs)).sum()),
-                          str(runs): int((nrun >= runs).sum())},
-            "per_s": perms / (perm_ms * 1e-3) if perm_ms > 0 else None,
-            # the adds run as FP32 pre-filter gathers (FP64 only near ties): the FLOP figure is
-            # the survey's normalisation, not the kernel's binding resource
-            "roofline": {"bound": "LDS / latency", "achieved": ach, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": ach / FP64_PEAK_TFLOPS, "kernel": "k_css_perm (HIP events)", "kernel_ms": perm_ms}}
+            "hist": [int((nrun <= 10).sum()), int(((nrun > 10) & (nrun <= 100)).sum()),
+                     int(((nrun > 100) & (nrun < runs)).sum()), int((nrun >= runs).sum())],
+            "per_s": perms / (perm_ms * 1e-3) if perm_ms > 0 else None, "kernel_ms": perm_ms}
+
+
+def timed_steps(env, fn, steps):
+    """Run fn() `steps` times, each bracketed by a barrier + sync; per step the max over
+    ranks.  Returns the list of step seconds."""
+    out = []
+    for k in range(steps):
+        env.sync()
+        t0 = time.perf_counter()
+        fn(k)
+        env.sync()
+        out.append(env.max_over_ranks(time.perf_counter() - t0))
+    return out
 
 
 def c3_leg(env, args, chroms, nch, windows, avals, bvals, apos, bpos, scores):
-    """configs[2] shape on the FET leg's resident chromosomes (20+20, runs=0)."""
+    """configs[2] shape on the FET leg's resident chromosomes (20+20, runs=0); median of
+    --css-steps timed steps."""
     torch, lib, _lib, check = env.torch, env.lib, env._lib, env.check
     pv = torch.zeros_like(scores)
+    kms = []
 
-    def step():
+    def step(_k):
         check(lib.gd_css_scan_device(env.ctx, chroms, nch, avals.data_ptr(), bvals.data_ptr(), apos.data_ptr(),
                                      bpos.data_ptr(), args.wsize, args.wstep, 10, 0, _lib.GD_WINDOWS_THREADED,
                                      scores.data_ptr(), pv.data_ptr(), env.stream))
+        kms.append(_lib.last_stage_ms()[1])  # bit planes -> scores (HIP events)
 
-    step()
-    env.sync()
-    t0 = time.perf_counter()
-    kms = 0.0
-    for _ in range(args.css_steps):
-        step()
-        kms += _lib.last_stage_ms()[1]  # bit planes -> scores (HIP events)
-    env.sync()
-    el = env.max_over_ranks(time.perf_counter() - t0)
-    kms /= args.css_steps
+    step(-1)
+    kms.clear()
+    ts = timed_steps(env, step, args.css_steps)
+    med = float(np.median(ts))
+    kmed = float(np.median(kms))
     m = args.asize + args.bsize
     flops = (4.0 / 3.0 * m ** 3 + 10.0 * m * m) * windows
-    ach = flops / (kms * 1e-3) / 1e12
-    out = {"metric": "CSS genomic windows/sec (classical MDS, runs=0; per-GPU batch)",
-           "value": windows * env.world * args.css_steps / el, "unit": "windows/s",
-           "ms_per_step": el * 1e3 / args.css_steps, "steps": args.css_steps,
-           "config": {"workload": f"CSS, configs[2] shape: {nch} chromosomes x {args.nsnp} SNPs per GPU, "
-                                  f"{args.asize}+{args.bsize} individuals, wsize {args.wsize}, wstep {args.wstep}, mcR=0",
-                      "windows_per_gpu": windows},
-           "roofline": {"bound": "fp64-valu", "achieved": ach, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                        "frac": ach / FP64_PEAK_TFLOPS, "traffic": None,
-                        "kernel": "k_css_pack + k_css_mds_p40 (HIP events)", "kernel_ms": kms,
-                        "alg_flops_per_window": flops / windows}}
-    v = css_valu("c3", windows, kms)
-    if v:
-        out["roofline"]["valu"] = v
+    out = {"value": windows * env.world / med, "unit": "windows/s", "ms_per_step": med * 1e3,
+           "ms_mean": float(np.mean(ts)) * 1e3, "steps": args.css_steps,
+           "workload": f"configs[2] shape: {nch} x {args.nsnp} SNPs per GPU, {args.asize}+{args.bsize}, runs=0",
+           "windows_per_gpu": windows, "kernel_ms": kmed,
+           "fp64_frac": flops / (kmed * 1e-3) / 1e12 / FP64_PEAK_TFLOPS, "alg_flops_per_window": flops / windows}
+    out.update(css_valu("c3", windows, kmed))
+    db = dist_build("c3", m, kmed, windows)
+    if db:
+        out["distance_build"] = db
     if env.rank == 0 and env.world == 1 and not args.no_cpu:
         out["cpu_baseline"] = css_cpu_baseline(args, args.asize, 10, 0)
     return out
@@ -522,107 +528,120 @@ def c3_leg(env, args, chroms, nch, windows, avals, bvals, apos, bpos, scores):
 
 def c45_leg(env, args, name, treshold, runs, queue):
     """configs[3] (runs=0, static shards) / configs[4] (mcR=1000, shared queue) per-GPU share:
-    args.c45_chroms chromosomes x 500k SNPs per GPU at 40+40; the (score, p) track of every
-    rank all-gathered into genome order after the timed steps (timed separately)."""
-    from gdscan.shard import default_store, gather_lists, gather_tracks, plan_shards, queue_pull
+    args.c45_chroms chromosomes x 500k SNPs per GPU at 40+40; median of --c45-steps timed
+    steps.  C4: each rank generates its plan_shards share once and scans it in one call.
+    C5: ranks pull chromosome tickets from a store counter and the input moves with the
+    ticket (queue_pull_pipelined): a rank generates only the chromosomes it pulls, into
+    two rotating slots, the next one on a side stream while the current one scans -- its
+    input memory is two chromosomes at any world size.  The (score, p) track of every
+    rank is gathered to rank 0 after the timed steps (timed separately)."""
+    from gdscan.shard import default_store, gather_lists, gather_tracks_to, plan_shards, queue_pull_pipelined
     torch, lib, _lib, check, synth = env.torch, env.lib, env._lib, env.check, env.synth
     pop, nsnp, world, rank = 40, args.nsnp, env.world, env.rank
     total = args.c45_chroms * world
     alen = nsnp * pop
-    shards = plan_shards([nsnp] * total, world)
-    resident = list(range(total)) if queue else shards[rank]
-    nres = len(resident)
-    av = torch.empty(nres * alen, dtype=torch.float64, device=env.dev)
-    bv = torch.empty(nres * alen, dtype=torch.float64, device=env.dev)
-    ap = torch.empty(nres * alen, dtype=torch.int32, device=env.dev)
-    bp = torch.empty(nres * alen, dtype=torch.int32, device=env.dev)
-    qtab = torch.from_numpy(synth.freq_table()).to(env.dev)
-    for i, c in enumerate(resident):
-        check(lib.gd_synth_device(1000 + c, nsnp, pop, pop, synth.MASTER_SEED, qtab.data_ptr(),
-                                  av.data_ptr() + i * alen * 8, bv.data_ptr() + i * alen * 8,
-                                  ap.data_ptr() + i * alen * 4, bp.data_ptr() + i * alen * 4, env.stream))
-    torch.cuda.synchronize()
-    last = ap.view(nres, alen)[:, -1].cpu().numpy().astype(np.int64)
-    reg_local = {c: int(last[i]) + 1 for i, c in enumerate(resident)}
-    if queue:
-        regends = [reg_local[c] for c in range(total)]
-    else:
-        got = gather_lists([reg_local[c] for c in resident]) if env.dist else [[reg_local[c] for c in resident]]
-        regends = [0] * total
-        for r, s in enumerate(shards):
-            for c, v in zip(s, got[r]):
-                regends[c] = v
+    regends = [synth.regend(1000 + c, nsnp) for c in range(total)]  # positions only (host)
     wins = [g // args.wstep for g in regends]
     wcount = [lib.gd_window_count(g, args.wsize, args.wstep, _lib.GD_WINDOWS_THREADED) for g in regends]
-    # descriptors of the resident chromosomes; queue: outputs at genome offsets, static: the
-    # rank's shard concatenated (gather_tracks' local layout)
     gofs = np.concatenate([[0], np.cumsum(wins)]).astype(np.int64)
-    chroms = (env.Chrom * nres)()
-    w = 0
-    for i, c in enumerate(resident):
-        d = chroms[i]
-        d.a_off = d.b_off = i * alen
+    shards = plan_shards([nsnp] * total, world)
+    nbuf = 2 if queue else len(shards[rank])
+    av = torch.empty(nbuf * alen, dtype=torch.float64, device=env.dev)
+    bv = torch.empty(nbuf * alen, dtype=torch.float64, device=env.dev)
+    ap = torch.empty(nbuf * alen, dtype=torch.int32, device=env.dev)
+    bp = torch.empty(nbuf * alen, dtype=torch.int32, device=env.dev)
+    qtab = torch.from_numpy(synth.freq_table()).to(env.dev)
+    gen = torch.cuda.Stream(env.dev)
+    ready = [torch.cuda.Event() for _ in range(nbuf)]
+
+    def generate(c, slot, stream):
+        check(lib.gd_synth_device(1000 + c, nsnp, pop, pop, synth.MASTER_SEED, qtab.data_ptr(),
+                                  av.data_ptr() + slot * alen * 8, bv.data_ptr() + slot * alen * 8,
+                                  ap.data_ptr() + slot * alen * 4, bp.data_ptr() + slot * alen * 4, stream))
+
+    def desc(slot, c, w_out, d):
+        d.a_off = d.b_off = slot * alen
         d.alen = d.blen = alen
         d.regend = regends[c]
-        d.w_out = int(gofs[c]) if queue else w
+        d.w_out = w_out
         d.seed = synth.MASTER_SEED + 1000 + c
-        w += wins[c]
-    nout = int(gofs[-1]) if queue else w
+
+    # outputs: genome order (queue) / the rank's shard concatenated (static, gather layout)
+    nout = int(gofs[-1]) if queue else sum(wins[c] for c in shards[rank])
     sc = torch.zeros(max(nout, 1), dtype=torch.float64, device=env.dev)
     pv = torch.zeros_like(sc)
-    stage = np.zeros(2)
-    my_windows = sum(wcount[c] for c in resident) if not queue else 0
+    stage = [0.0, 0.0]
+    one = (env.Chrom * 1)()
 
-    def scan(idx, n):
-        ptr = ctypes.cast(ctypes.addressof(chroms) + idx * ctypes.sizeof(env.Chrom), ctypes.POINTER(env.Chrom))
-        check(lib.gd_css_scan_device(env.ctx, ptr, n, av.data_ptr(),
-                                     bv.data_ptr(), ap.data_ptr(), bp.data_ptr(), args.wsize, args.wstep, treshold,
-                                     runs, _lib.GD_WINDOWS_THREADED, sc.data_ptr(), pv.data_ptr(), env.stream))
+    def scan(ch, n):
+        check(lib.gd_css_scan_device(env.ctx, ch, n, av.data_ptr(), bv.data_ptr(), ap.data_ptr(), bp.data_ptr(),
+                                     args.wsize, args.wstep, treshold, runs, _lib.GD_WINDOWS_THREADED,
+                                     sc.data_ptr(), pv.data_ptr(), env.stream))
         st = _lib.last_stage_ms()
         stage[0] += st[1]
         stage[1] += st[2]
 
+    if not queue:
+        mine = shards[rank]
+        chroms = (env.Chrom * len(mine))()
+        w = 0
+        for i, c in enumerate(mine):
+            generate(c, i, env.stream)
+            desc(i, c, w, chroms[i])
+            w += wins[c]
+        torch.cuda.synchronize()
     store = default_store() if (queue and env.dist) else None
     tick = [0]
 
+    def prepare(c, slot):
+        generate(c, slot, gen.cuda_stream)
+        ready[slot].record(gen)
+
+    def work(c, slot):
+        torch.cuda.current_stream(env.dev).wait_event(ready[slot])
+        desc(slot, c, int(gofs[c]), one[0])
+        scan(one, 1)  # returns after the scan's stream sync: the slot is free again
+
+    class Local:  # one rank without a process group: the queue is the chromosome order
+        def __init__(self):
+            self.n = {}
+
+        def add(self, key, v):
+            self.n[key] = self.n.get(key, 0) + v
+            return self.n[key]
+
+    local_store = Local()
+
+    done_last = []
+
     def step(k):
+        nonlocal done_last
         if not queue:
-            scan(0, nres)
-            return list(resident)
-        if store is None:  # one rank: the queue is the chromosome order
-            for c in range(total):
-                scan(c, 1)
-            return list(range(total))
-        done = queue_pull(store, f"gd_{name}_{k}", total, lambda c: scan(c, 1))
-        return done
+            scan(chroms, len(shards[rank]))
+            done_last = list(shards[rank])
+        else:
+            done_last = queue_pull_pipelined(store if store is not None else local_store, f"gd_{name}_{k}", total,
+                                             prepare, work)
 
     step(-1)  # warmup (sizes the workspace)
     env.sync()
-    stage[:] = 0
-    busy = []
-    done = []
-    t0 = time.perf_counter()
-    for k in range(args.c45_steps):
-        b0 = time.perf_counter()
-        done = step(k)
-        busy.append(time.perf_counter() - b0)
-    env.sync()
-    el = env.max_over_ranks(time.perf_counter() - t0)
-    stage /= args.c45_steps
+    stage[:] = [0.0, 0.0]
+    ts = timed_steps(env, step, args.c45_steps)
+    stage = [x / args.c45_steps for x in stage]
+    med = float(np.median(ts))
     all_windows = sum(wcount)
-    out = {"metric": f"CSS genomic windows/sec ({'configs[4]: mcT=10, mcR=1000' if runs else 'configs[3]: runs=0'}; "
-                     f"{args.c45_chroms} chromosomes per GPU)",
-           "value": all_windows * args.c45_steps / el, "unit": "windows/s", "n_gpus": world,
-           "ms_per_step": el * 1e3 / args.c45_steps, "steps": args.c45_steps,
-           "config": {"workload": f"{total} chromosomes x {nsnp} SNPs ({args.c45_chroms} per GPU), 40+40, "
-                                  f"wsize {args.wsize}, wstep {args.wstep}, mcT={treshold}, mcR={runs}",
-                      "windows": all_windows,
-                      "sharding": "shared chromosome queue (store counter), inputs resident on every rank"
-                      if queue else "plan_shards (LPT by SNP count), whole chromosomes per rank"}}
-    # the one collective: (score, p) of every rank's chromosomes, all-gathered in genome order
+    mine = done_last
+    mine_w = sum(wcount[c] for c in mine)
+    out = {"value": all_windows / med, "unit": "windows/s", "n_gpus": world, "ms_per_step": med * 1e3,
+           "ms_mean": float(np.mean(ts)) * 1e3, "steps": args.c45_steps,
+           "workload": f"{total} chromosomes x {nsnp} SNPs ({args.c45_chroms} per GPU), 40+40, mcT={treshold}, "
+                       f"mcR={runs}", "windows": all_windows,
+           "sharding": "store-counter ticket queue, input generated per pulled ticket (2 slots)" if queue
+           else "plan_shards (LPT by SNP count), whole chromosomes per rank",
+           "resident_input_bytes_per_rank": int(nbuf * alen * 24)}
+    # the one collective: (score, p) of every rank's chromosomes, gathered to rank 0
     if env.dist:
-        shard_done = gather_lists(done) if queue else shards
-        mine = shard_done[rank]
+        shard_done = gather_lists(mine) if queue else shards
         if queue:
             local = torch.cat([torch.stack([sc[gofs[c]:gofs[c + 1]], pv[gofs[c]:gofs[c + 1]]], 1) for c in mine]) \
                 if mine else torch.zeros((0, 2), dtype=torch.float64, device=env.dev)
@@ -630,33 +649,27 @@ def c45_leg(env, args, name, treshold, runs, queue):
             local = torch.stack([sc[:nout], pv[:nout]], 1)
         env.sync()
         g0 = time.perf_counter()
-        track = gather_tracks(local.to(env.cdev), shard_done, wins)
+        track = gather_tracks_to(local.to(env.cdev), shard_done, wins, dst=0)
         torch.cuda.synchronize()
         out["track_gather_ms"] = env.max_over_ranks((time.perf_counter() - g0) * 1e3)
-        sc_all, p_all = track[:, 0], track[:, 1]
-        busy_all = gather_lists([int(1e6 * sum(busy))])
-        per_rank = [b[0] * 1e-6 for b in busy_all]
-        out["per_rank_busy_s"] = per_rank
-        out["imbalance"] = max(per_rank) / (sum(per_rank) / len(per_rank))
         if queue:
-            out["chromosomes_per_rank"] = [len(s) for s in shard_done]
+            out["chromosomes_per_rank"] = [len(x) for x in shard_done]
+        if rank != 0:
+            return out
+        sc_all, p_all = track[:, 0], track[:, 1]
     else:
         sc_all, p_all = sc[:nout], pv[:nout]
-        out["track_gather_ms"] = None
     pm, sm = p_all.cpu().numpy(), sc_all.cpu().numpy()
     computed = sm != 0
     m = 2 * pop
     flops = (4.0 / 3.0 * m ** 3 + 10.0 * m * m)
-    # per-rank kernel time of the MDS stage over the windows this rank scanned
-    mine_w = sum(wcount[c] for c in done) if queue else my_windows
-    ach = flops * mine_w / (stage[0] * 1e-3) / 1e12 if stage[0] > 0 else 0.0
-    out["roofline"] = {"bound": "fp64-valu", "achieved": ach, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                       "frac": ach / FP64_PEAK_TFLOPS, "kernel": "k_css_pack + k_css_mds_t80 (HIP events, rank 0)",
-                       "kernel_ms": float(stage[0]), "alg_flops_per_window": flops}
-    v = css_valu("c4", mine_w, float(stage[0]))
-    if v:
-        out["roofline"]["valu"] = v
-    out["stage_ms"] = {"planes_mds": float(stage[0]), "permutations": float(stage[1])}
+    out["kernel_ms"] = float(stage[0])
+    out["fp64_frac"] = flops * mine_w / (stage[0] * 1e-3) / 1e12 / FP64_PEAK_TFLOPS if stage[0] > 0 else 0.0
+    out.update(css_valu("c4", mine_w, float(stage[0])))
+    if not runs:
+        db = dist_build("c4", m, float(stage[0]), mine_w)
+        if db:
+            out["distance_build"] = db
     out["mean_p"] = float(pm[computed].mean()) if computed.any() else None
     if runs > 0 and computed.any():
         perm_ms = float(stage[1])
@@ -666,18 +679,12 @@ def c45_leg(env, args, name, treshold, runs, queue):
             perm_ms = float(t.item())
         out["permutations"] = perm_stats(pm, computed, treshold, runs, perm_ms, pop)
         pv_ = css_valu("c5_perm", mine_w, float(stage[1]))
-        if pv_:
-            out["permutations"]["valu"] = pv_
+        out["permutations"].update(pv_)
         doc = json.loads(CSS_VALU_FILE.read_text()).get("c5_perm", {}) if CSS_VALU_FILE.exists() else {}
         if "mfma" in doc and stage[1] > 0:
-            # matrix-core share of the permutation kernel (score_mfma): MFMA busy SIMD-cycles per
-            # window (committed PMC profile) x this rank's windows over its SIMD-cycles at 2.4 GHz
             mf = doc["mfma"]
             busy = mf["busy_simd_cycles_per_dispatch"] / doc["windows_per_dispatch"] * mine_w
-            out["permutations"]["mfma"] = {
-                "instruction": "v_mfma_f32_32x32x16_f16", "busy_frac": busy / (1024 * 2.4e9 * stage[1] * 1e-3),
-                "mfma_per_window": mf["mfma_per_dispatch"] / doc["windows_per_dispatch"],
-                "source": f"{CSS_VALU_FILE.relative_to(ROOT)} [c5_perm.mfma] ({mf['method']})"}
+            out["permutations"]["mfma_busy"] = busy / (1024 * 2.4e9 * stage[1] * 1e-3)
     if env.rank == 0 and env.world == 1 and not args.no_cpu:
         out["cpu_baseline"] = css_cpu_baseline(args, pop, treshold, runs)
     del av, bv, ap, bp
@@ -687,25 +694,51 @@ def c45_leg(env, args, name, treshold, runs, queue):
 # ----------------------------------------------------------------------------- dry run (CPU)
 def dry_run(args, rank, world, dist):
     """The distributed plumbing without a GPU: shard plan, the chromosome queue over the
-    default store, and the track gather (gloo), checked against the expected genome order."""
+    default store with the input moving with the ticket (queue_pull_pipelined: a rank
+    materialises only what it pulls, at most two tickets at a time), the all-gather and the
+    gather-to-rank-0 of the track (gloo), checked against the expected genome order."""
     import torch
-    from gdscan.shard import default_store, gather_lists, gather_tracks, plan_shards, queue_pull
+    from gdscan.shard import (default_store, gather_lists, gather_tracks, gather_tracks_to, plan_shards,
+                              queue_pull_pipelined)
     total = args.c45_chroms * world
     wins = [100 + 7 * c for c in range(total)]
     offs = np.concatenate([[0], np.cumsum(wins)])
     store = default_store()
-    done = queue_pull(store, "gd_dry", total, lambda c: time.sleep(0.001 * (1 + c % 3)))
+    slots = {}
+    made = []
+    peak = [0]
+
+    def prepare(c, slot):  # the "input" of ticket c: its window indices, produced only when pulled
+        slots[slot] = (c, torch.arange(offs[c], offs[c + 1], dtype=torch.float64))
+        made.append(c)
+        peak[0] = max(peak[0], len(slots))
+
+    parts = {}
+
+    def work(c, slot):
+        cc, data = slots[slot]
+        assert cc == c
+        time.sleep(0.001 * (1 + c % 3))
+        parts[c] = torch.stack([data, data], 1)
+
+    done = queue_pull_pipelined(store, "gd_dry", total, prepare, work)
     lists = gather_lists(done)
     assert sorted(c for s in lists for c in s) == list(range(total))
-    local = torch.cat([torch.stack([torch.arange(offs[c], offs[c + 1], dtype=torch.float64)] * 2, 1) for c in done]) \
-        if done else torch.zeros((0, 2), dtype=torch.float64)
+    local = torch.cat([parts[c] for c in done]) if done else torch.zeros((0, 2), dtype=torch.float64)
+    want = torch.arange(offs[-1], dtype=torch.float64)
     track = gather_tracks(local, lists, wins)
-    ok = bool(torch.equal(track[:, 0], torch.arange(offs[-1], dtype=torch.float64)))
+    ok = bool(torch.equal(track[:, 0], want))
+    t0 = gather_tracks_to(local, lists, wins, dst=0)
+    ok0 = bool(torch.equal(t0[:, 1], want)) if rank == 0 else t0 is None
+    ok0 = gather_lists([int(ok0)])
+    made_all = gather_lists(made)
     shards = plan_shards([args.nsnp] * total, world)
     if rank == 0:
         print(json.dumps({"dry_run": True, "n_gpus": world, "backend": args.backend, "queue_per_rank":
-                          [len(s) for s in lists], "static_per_rank": [len(s) for s in shards], "gather_ok": ok}),
-              flush=True)
+                          [len(s) for s in lists], "static_per_rank": [len(s) for s in shards], "gather_ok": ok,
+                          "gather_to_0_ok": all(x[0] == 1 for x in ok0),
+                          "materialised_only_pulled": all(sorted(m) == sorted(d) for m, d in zip(made_all, lists)),
+                          "max_live_inputs": peak[0]}), flush=True)
     dist.barrier()
 
 
@@ -733,14 +766,22 @@ def main():
     # more ranks than GPUs (a rehearsal of --gpus N on a smaller box): ranks share the
     # devices round-robin, and the collectives go over gloo (RCCL refuses two ranks on one
     # GPU); device_count() does not initialise the GPU
+    from gdscan.shard import choose_backend
     ndev = max(1, torch.cuda.device_count())
-    shared = world > ndev
-    if shared and args.backend == "nccl":
-        args.backend = "gloo"
+    args.backend, _on_device = choose_backend(world, ndev, args.backend)
     local = local % ndev
     torch.cuda.set_device(local)
-    if world > 1:
+    if world > 1 or args.force_dist:
         import torch.distributed as dist_mod
+        if world == 1:  # --force-dist: a one-rank group, so the collectives really run (RCCL on the GPU)
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            if "MASTER_PORT" not in os.environ:
+                sk = socket.socket()
+                sk.bind(("127.0.0.1", 0))
+                os.environ["MASTER_PORT"] = str(sk.getsockname()[1])
+                sk.close()
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
         if args.backend == "gloo":
             dist_mod.init_process_group("gloo")
         else:
@@ -803,7 +844,7 @@ def main():
     if dist:
         # the one collective of the path: all ranks' (score, stddev) tracks gathered in
         # genome order; measured once, outside the timed steps
-        from gdscan.shard import gather_tracks
+        from gdscan.shard import gather_tracks_to
         wt = torch.zeros(world * nch, dtype=torch.int64, device=env.cdev)
         wt[rank * nch:(rank + 1) * nch] = torch.tensor([chroms[c].regend // args.wstep for c in range(nch)])
         dist.all_reduce(wt)  # every rank learns every chromosome's window count
@@ -811,7 +852,7 @@ def main():
         loc = torch.stack([scores, stddev], 1)
         env.sync()
         g0 = time.perf_counter()
-        gather_tracks(loc.to(env.cdev), shards, wt.tolist())
+        gather_tracks_to(loc.to(env.cdev), shards, wt.tolist(), dst=0)
         torch.cuda.synchronize()
         gather_ms = env.max_over_ranks((time.perf_counter() - g0) * 1e3)
     total_windows = windows * world
@@ -820,6 +861,29 @@ def main():
     kernel_ms = float(stage[_lib.GD_NSTAGES - 1])  # first kernel -> last kernel of the scan
     alg_bytes = 12.0 * (nch * (alen + blen)) + 16.0 * windows
     achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
+    sources = {}
+    roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "traffic": None, "alg_bytes_per_step": alg_bytes,
+            "kernel_ms": kernel_ms, "kernel": "whole scan: k_popsize, k_bounds, k_fet_window_fast (HIP events)"}
+    if TRAFFIC_FILE.exists():
+        tr = json.loads(TRAFFIC_FILE.read_text())
+        if tr.get("config") == [nch, nsnp, a, b]:
+            roof["traffic"] = tr["bytes_per_scan"]
+            sources["traffic"] = f"{TRAFFIC_FILE.relative_to(ROOT)}: {tr['method']}"
+    if VALU_FILE.exists():
+        # what binds the scan: VALU issue (the bootstrap's nrand48 draws), not HBM --
+        # wave-instructions per scan (PMC SQ_INSTS_VALU, committed profile) over this run's
+        # scan time against one wave64 instruction per SIMD per 4 cycles, and the window
+        # kernel's own VALU busy fraction from its SQ counters
+        vr = json.loads(VALU_FILE.read_text())
+        if vr.get("config") == [nch, nsnp, a, b]:
+            roof["valu_ginsts"] = vr["valu_wave_insts_per_scan"] / (kernel_ms * 1e-3) / 1e9
+            roof["valu_issue_peak_ginsts"] = VALU_ISSUE_GINSTS
+            roof["valu_frac"] = roof["valu_ginsts"] / VALU_ISSUE_GINSTS
+            roof["valu_insts_per_scan"] = vr["valu_wave_insts_per_scan"]
+            if "window_kernel_valu_busy" in vr:
+                roof["window_kernel_valu_busy"] = vr["window_kernel_valu_busy"]
+            sources["valu"] = f"{VALU_FILE.relative_to(ROOT)}: {vr['method']}"
     out = {
         "metric": "FET genomic windows/sec (10M SNPs, 20+20 indiv, 2.5 kb windows; per-GPU batch)",
         "value": value,
@@ -834,46 +898,20 @@ def main():
         "dtype": "f64",
         "data": "synthetic (seeded generator, SURVEY.md 8(d)), generated on device",
         "config": {
-            "workload": "FET genome-wide, configs[1]: 20 chromosomes x 500k SNPs per GPU, 20+20 individuals, "
-                        "wsize 2500, wstep 500, perc 0.95, 100 bootstrap replicates",
+            "workload": "FET configs[1]: 20 x 500k SNPs per GPU, 20+20, wsize 2500, wstep 500, perc 0.95, 100 reps",
             "chromosomes_per_gpu": nch, "snps_per_gpu": nch * nsnp, "windows_per_gpu": windows,
             "asize": a, "bsize": b, "parallelism": f"window-sharded x{world} (whole chromosomes per rank)",
-            "ranks_per_gpu": -(-world // ndev), "collective_backend": args.backend if world > 1 else None,
+            "ranks_per_gpu": -(-world // ndev), "collective_backend": args.backend if dist else None,
             "track_gather_ms": gather_ms,
         },
-        "roofline": {
-            "bound": "hbm",
-            "achieved": achieved,
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS,
-            "traffic": None,
-            "kernel": "whole scan pipeline (k_popsize, k_bounds, k_fet_window_fast; k_snp_fet / k_fet_lut_* when "
-                      "the score table is cold), HIP events on the scan's streams per step",
-            "alg_bytes_per_step": alg_bytes,
-            "stage_ms": {"hbm_passes_done": stage[0], "fast_windows_done": stage[1],
-                         "general_path": stage[2], "scan_total": stage[3]},
-        },
+        "roofline": roof,
     }
-    if TRAFFIC_FILE.exists():
-        tr = json.loads(TRAFFIC_FILE.read_text())
-        if tr.get("config") == [nch, nsnp, a, b]:
-            out["roofline"]["traffic"] = tr["bytes_per_scan"]
-            out["roofline"]["traffic_source"] = f"{TRAFFIC_FILE.relative_to(ROOT)} ({tr['method']})"
-    if VALU_FILE.exists():
-        # the binding resource of the scan: VALU issue (the bootstrap's nrand48 draws), not
-        # HBM -- wave-instructions per scan (PMC SQ_INSTS_VALU, committed profile) over this
-        # run's scan time, against the measured VALU issue peak
-        vr = json.loads(VALU_FILE.read_text())
-        if vr.get("config") == [nch, nsnp, a, b]:
-            peak, src = valu_peak()
-            ginst = vr["valu_wave_insts_per_scan"] / (stage[3] * 1e-3) / 1e9
-            out["roofline"]["valu"] = {
-                "bound": "valu-issue", "achieved": ginst, "peak": peak, "unit": "G wave-insts/s",
-                "frac": ginst / peak, "insts_per_scan": vr["valu_wave_insts_per_scan"],
-                "source": f"{VALU_FILE.relative_to(ROOT)} ({vr['method']}); peak: {src}"}
     if rank == 0 and world == 1 and not args.no_cpu:
-        out["cpu_baseline"] = fet_cpu_baseline(args, scores, chroms)
+        cb = fet_cpu_baseline(args, scores, chroms)
+        sources["cpu_baseline"] = cb.pop("what")
+        out["cpu_baseline"] = cb
+    out["stage_ms"] = {"hbm_passes_done": float(stage[0]), "fast_windows_done": float(stage[1]),
+                       "general_path": float(stage[2]), "scan_total": float(stage[3])}
 
     if not args.no_extra:
         out["regions"] = regions_run(args, scores, stddev, chroms, nch, rank, world, dev)
@@ -885,16 +923,25 @@ def main():
         del codes
 
     if not args.no_css:
-        out["css"] = c3_leg(env, args, chroms, nch, windows, avals, bvals, apos, bpos, scores)
+        css = {"c3": c3_leg(env, args, chroms, nch, windows, avals, bvals, apos, bpos, scores)}
         del avals, bvals, apos, bpos, scores, stddev
         torch.cuda.empty_cache()
         if not args.no_c45:
-            out["css"]["c4"] = c45_leg(env, args, "c4", 10, 0, queue=False)
+            css["c4"] = c45_leg(env, args, "c4", 10, 0, queue=False)
             torch.cuda.empty_cache()
-            out["css"]["c5"] = c45_leg(env, args, "c5", 10, 1000, queue=True)
+            css["c5"] = c45_leg(env, args, "c5", 10, 1000, queue=True)
+        out["css"] = css
+        if CSS_VALU_FILE.exists():
+            sources["css_valu"] = f"{CSS_VALU_FILE.relative_to(ROOT)} (SQ_INSTS_VALU per window; busy = " \
+                                  "SQ_ACTIVE_INST_VALU x 4 cycles / SIMD-cycles)"
+        if CSS_PHASE_FILE.exists():
+            sources["distance_build"] = f"{CSS_PHASE_FILE.relative_to(ROOT)} (GD_CSS_PROFILE phase cycles, " \
+                                        "k_css_pack share from the kernel trace)"
+        sources["css_cpu"] = "oracle/css_oracle.c threaded over the host cores (the reference CSS needs GSL, absent)"
     lib.gd_ctx_destroy(ctx)
+    out["sources"] = sources
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        print(json.dumps(out, separators=(",", ":")), flush=True)
     if dist:
         dist.barrier()
         dist.destroy_process_group()

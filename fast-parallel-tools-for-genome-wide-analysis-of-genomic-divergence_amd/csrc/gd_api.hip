@@ -74,7 +74,10 @@ int gd_synth_launch(int chrom, int nsnp, int asize, int bsize, uint64_t seed, co
 
 /* ------------------------------------------------------------------ errors */
 static thread_local std::string g_err;
-static std::atomic<uint64_t> g_seed{GD_DEFAULT_SEED};
+/* seed of the reference-signature entry points: per calling thread (gd_set_seed affects
+ * only the thread that calls it; every thread starts at GD_DEFAULT_SEED), so two threads
+ * that each set a seed and call fisher_exact_tester cannot race on it */
+static thread_local uint64_t g_seed = GD_DEFAULT_SEED;
 static std::atomic<int> g_fet_mode{GD_FET_REFERENCE};
 static thread_local float g_stage_ms[GD_NSTAGES];
 
@@ -613,7 +616,7 @@ static int host_scan(const double *avals, const double *bvals, const int *apos, 
   ch.alen = alen;
   ch.blen = blen;
   ch.regend = regend;
-  ch.seed = g_seed.load();
+  ch.seed = g_seed;
   st = run(ctx, &ch, av, bv, ap, bp, o0, o1, s);
   if (st) return st;
   if (nwin > 0) {
@@ -748,7 +751,7 @@ extern "C" int gd_fet_threadcompute(const double *avals, const double *bvals, co
                                     int regstart, int regend, int wsize, int wstep, int alen, int blen,
                                     double perc, double *scores, double *stddev) {
   (void)regstart; /* ignored by the reference too (threadfisher.c:110) */
-  return gd_fet_scan_host(avals, bvals, apos, bpos, regend, wsize, wstep, alen, blen, perc, g_seed.load(),
+  return gd_fet_scan_host(avals, bvals, apos, bpos, regend, wsize, wstep, alen, blen, perc, g_seed,
                           GD_WINDOWS_THREADED, scores, stddev);
 }
 
@@ -756,7 +759,7 @@ extern "C" int gd_fet_compute(const double *avals, const double *bvals, const in
                               int regstart, int regend, int wsize, int wstep, int alen, int blen, double perc,
                               double *scores, double *stddev) {
   (void)regstart; /* ignored by the reference too (cFisher.c:60) */
-  return gd_fet_scan_host(avals, bvals, apos, bpos, regend, wsize, wstep, alen, blen, perc, g_seed.load(),
+  return gd_fet_scan_host(avals, bvals, apos, bpos, regend, wsize, wstep, alen, blen, perc, g_seed,
                           GD_WINDOWS_SERIAL, scores, stddev);
 }
 
@@ -978,7 +981,7 @@ extern "C" int gd_css_threadcompute(const double *avals, const double *bvals, co
                                     int treshold, int runs, int drosophila, int mds, double *scores, double *p) {
   (void)regstart; /* ignored by the reference too (threadcss.c) */
   return gd_css_scan_host_ex(avals, bvals, apos, bpos, regend, wsize, wstep, alen, blen, treshold, runs, drosophila,
-                             mds, g_seed.load(), GD_WINDOWS_THREADED, scores, p);
+                             mds, g_seed, GD_WINDOWS_THREADED, scores, p);
 }
 
 extern "C" int gd_css_compute(const double *avals, const double *bvals, const int *apos, const int *bpos,
@@ -986,12 +989,12 @@ extern "C" int gd_css_compute(const double *avals, const double *bvals, const in
                               int runs, int drosophila, int mds, double *scores, double *p) {
   (void)regstart; /* ignored by the reference too (css.c:78) */
   return gd_css_scan_host_ex(avals, bvals, apos, bpos, regend, wsize, wstep, alen, blen, treshold, runs, drosophila,
-                             mds, g_seed.load(), GD_WINDOWS_SERIAL, scores, p);
+                             mds, g_seed, GD_WINDOWS_SERIAL, scores, p);
 }
 
 /* ------------------------------------------------------------- utilities */
-extern "C" void gd_set_seed(uint64_t seed) { g_seed.store(seed); }
-extern "C" uint64_t gd_get_seed(void) { return g_seed.load(); }
+extern "C" void gd_set_seed(uint64_t seed) { g_seed = seed; }
+extern "C" uint64_t gd_get_seed(void) { return g_seed; }
 /* ------------------------------------------------------------ packed tracks */
 extern "C" int gd_fet_scan_packed_device(gd_ctx *ctx, const gd_pchrom *chroms, int nchrom, const uint64_t *acodes,
                                          const uint64_t *bcodes, const int32_t *rowpos, int wsize, int wstep,

@@ -61,11 +61,21 @@ def freq_table() -> np.ndarray:
     return np.sin(np.pi * u / 2.0) ** 2
 
 
+def positions(c: int, nsnp: int, seed: int = MASTER_SEED) -> np.ndarray:
+    """SNP positions of chromosome c (one per row), as chromosome() places them."""
+    s = np.arange(nsnp, dtype=np.uint64)
+    return np.cumsum(1 + (_h(seed, c, s, TAG_GAP) % np.uint64(99)).astype(np.int64))
+
+
+def regend(c: int, nsnp: int, seed: int = MASTER_SEED) -> int:
+    """chromosome(c, ...)[4] without generating the genotypes (last position + 1)."""
+    return int(positions(c, nsnp, seed)[-1]) + 1
+
+
 def chromosome(c: int, nsnp: int, asize: int, bsize: int, seed: int = MASTER_SEED):
     """Return (avals, bvals, apos, bpos, regend) for chromosome c."""
     s = np.arange(nsnp, dtype=np.uint64)
-    gap = 1 + (_h(seed, c, s, TAG_GAP) % np.uint64(99)).astype(np.int64)
-    pos = np.cumsum(gap)
+    pos = positions(c, nsnp, seed)
     if pos[-1] >= 2**31 - 1:
         raise ValueError("chromosome too long for int32 positions")
     qtab = freq_table()

@@ -20,7 +20,8 @@
  *
  * Reproducibility: the reference seeds its bootstrap / permutation RNG from
  * time(NULL); here every window w draws from its own nrand48 stream seeded by
- * (seed, w) (gd_set_seed, default GD_DEFAULT_SEED), so stddev and p are
+ * (seed, w) (gd_set_seed, default GD_DEFAULT_SEED; the seed is per calling
+ * thread, so concurrent callers do not share it), so stddev and p are
  * deterministic.  Scores do not depend on the seed.
  *
  * libgdscan_fisher.so / libgdscan_css.so additionally export the reference's own
@@ -231,8 +232,9 @@ int gd_merge_regions(gd_ctx *ctx, const double *vals, const int32_t *seq, const 
                      int64_t *region_end, int64_t *nregions, int64_t *nselected, void *hip_stream);
 
 /* ---- configuration / diagnostics ---- */
-void gd_set_seed(uint64_t seed);     /* seed used by the reference-signature entry points */
-uint64_t gd_get_seed(void);
+void gd_set_seed(uint64_t seed);     /* seed used by the reference-signature entry points called from the
+                                       calling thread (thread-local; every thread starts at GD_DEFAULT_SEED) */
+uint64_t gd_get_seed(void);          /* the calling thread's seed */
 const char *gd_last_error(void);     /* thread-local message for the last failing call */
 int gd_device_count(void);
 

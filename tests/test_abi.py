@@ -51,3 +51,30 @@ def test_no_gpu_errors_cleanly():
     av, bv, ap, bp, regend = synth.chromosome(0, 3000, 4, 4)
     with pytest.raises(GdError):
         fet.scan(av, bv, ap, bp, regend)
+
+
+def test_seed_is_per_thread():
+    """gd_set_seed (the seed of the reference-signature entry points) affects only the
+    calling thread, so two threads that each set a seed and then call fisher_exact_tester
+    cannot race on it (no GPU call: set/get only)."""
+    import threading
+    from gdscan._lib import GD_DEFAULT_SEED, lib
+    got = {}
+    gate = threading.Barrier(2)
+
+    def worker(name, seed):
+        lib.gd_set_seed(seed)
+        gate.wait()  # both threads have set their seed before either reads it back
+        got[name] = lib.gd_get_seed()
+
+    ts = [threading.Thread(target=worker, args=(k, s)) for k, s in (("a", 11), ("b", 22))]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert got == {"a": 11, "b": 22}
+    fresh = {}
+    t = threading.Thread(target=lambda: fresh.setdefault("s", lib.gd_get_seed()))
+    t.start()
+    t.join()
+    assert fresh["s"] == GD_DEFAULT_SEED

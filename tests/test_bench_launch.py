@@ -1,7 +1,8 @@
 """CPU: bench.py's launcher and distributed plumbing without a GPU.  `bench.py --gpus 2`
 with no torch.distributed environment starts torch.distributed.run itself (before any GPU
 call); --backend gloo --dry-run then runs the shard plan, the shared chromosome queue over
-the default store (the C5 leg's load balancing) and the (score, p) track gather."""
+the default store (the C5 leg's load balancing, its input produced per pulled ticket) and the
+(score, p) track gathers (all-gather and gather to rank 0)."""
 import json
 import os
 import subprocess
@@ -19,8 +20,10 @@ def test_bench_spawns_ranks_and_gathers():
     lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
     assert len(lines) == 1, r.stdout
     out = lines[0]
-    assert out["dry_run"] and out["n_gpus"] == 2 and out["gather_ok"]
+    assert out["dry_run"] and out["n_gpus"] == 2 and out["gather_ok"] and out["gather_to_0_ok"]
     assert sum(out["queue_per_rank"]) == 8 and out["static_per_rank"] == [4, 4]
+    # the C5 queue moves the input with the ticket: only pulled chromosomes are made, two at a time
+    assert out["materialised_only_pulled"] and out["max_live_inputs"] <= 2
 
 
 def test_bench_single_rank_needs_no_launcher():

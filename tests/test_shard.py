@@ -78,3 +78,82 @@ def test_gather_tracks_gloo_world2(oracle):
         p.join(timeout=300)
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
     assert q.get(timeout=10) is True
+
+
+def test_choose_backend():
+    """RCCL with device tensors when every rank has its own GPU; gloo on host tensors when
+    ranks must share devices (RCCL refuses two ranks on one GPU) or gloo is asked for."""
+    from gdscan.shard import choose_backend
+    assert choose_backend(8, 8) == ("nccl", True)
+    assert choose_backend(1, 1) == ("nccl", True)
+    assert choose_backend(2, 1) == ("gloo", False)
+    assert choose_backend(4, 8, "gloo") == ("gloo", False)
+    assert choose_backend(1, 0) == ("nccl", True)  # one rank, GPU count unknown before init
+
+
+class _Store:
+    def __init__(self):
+        self.v = {}
+
+    def add(self, key, n):
+        self.v[key] = self.v.get(key, 0) + n
+        return self.v[key]
+
+
+def test_queue_pull_pipelined_prefetches_next_ticket():
+    """The input moves with the ticket: ticket t + 1 is prepared before t is worked on,
+    never more than `slots` inputs are alive, and a slot is reused only after its scan."""
+    from gdscan.shard import queue_pull_pipelined
+    events, live = [], {}
+
+    def prepare(c, slot):
+        assert slot not in live, "slot overwritten while its ticket is still unscanned"
+        live[slot] = c
+        events.append(("prep", c, slot))
+
+    def work(c, slot):
+        assert live.pop(slot) == c
+        events.append(("work", c, slot))
+
+    done = queue_pull_pipelined(_Store(), "k", 5, prepare, work)
+    assert done == [0, 1, 2, 3, 4]
+    assert events[:3] == [("prep", 0, 0), ("prep", 1, 1), ("work", 0, 0)]
+    assert [e for e in events if e[0] == "work"] == [("work", c, c % 2) for c in range(5)]
+    assert queue_pull_pipelined(_Store(), "k", 0, prepare, work) == []
+
+
+def _worker_to0(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+    from gdscan.shard import gather_tracks, gather_tracks_to
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    wins = [5, 0, 7, 3, 4]
+    shards = [[0, 3], [1, 2, 4]]
+    offs = np.concatenate([[0], np.cumsum(wins)])
+    local = torch.cat([torch.stack([torch.arange(offs[c], offs[c + 1], dtype=torch.float64),
+                                    -torch.arange(offs[c], offs[c + 1], dtype=torch.float64)], 1)
+                       for c in shards[rank]])
+    t0 = gather_tracks_to(local, shards, wins, dst=0)
+    ta = gather_tracks(local, shards, wins)
+    want = torch.arange(offs[-1], dtype=torch.float64)
+    if rank == 0:
+        q.put(bool(torch.equal(t0[:, 0], want) and torch.equal(t0[:, 1], -want) and torch.equal(t0, ta)))
+    else:
+        q.put(t0 is None)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gather_tracks_to_rank0_gloo_world2():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_to0, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=120)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    assert q.get(timeout=10) is True and q.get(timeout=10) is True

@@ -82,3 +82,26 @@ def test_two_ranks_scan_shards_and_gather():
             p.join()
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
     assert q.get(timeout=10) == {"fet": True, "css": True}
+
+
+def test_rccl_device_tensor_gathers_one_rank():
+    """The RCCL branch on device tensors: bench.py --force-dist runs a one-rank "nccl"
+    process group on cuda:0 (init_process_group with device_id, the track all-reduce and
+    gather-to-rank-0 of the FET leg and of the C4/C5 legs on device tensors), the same code
+    the 8-GPU node runs, on a small genome."""
+    import json
+    import subprocess
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parent.parent
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env["MASTER_ADDR"] = "127.0.0.1"
+    r = subprocess.run([sys.executable, str(root / "bench.py"), "--force-dist", "--steps", "2", "--warmup", "1",
+                        "--nchrom", "2", "--nsnp", "60000", "--no-cpu", "--no-extra", "--css-steps", "1",
+                        "--c45-chroms", "2", "--c45-steps", "1"], capture_output=True, text=True, timeout=240,
+                       env=env, cwd=root)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out["config"]["collective_backend"] == "nccl" and out["config"]["track_gather_ms"] is not None
+    assert out["css"]["c4"]["track_gather_ms"] is not None and out["css"]["c5"]["track_gather_ms"] is not None
+    assert out["css"]["c5"]["resident_input_bytes_per_rank"] == 2 * 60000 * 40 * 24
