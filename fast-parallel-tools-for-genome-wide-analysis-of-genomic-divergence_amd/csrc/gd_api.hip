@@ -53,6 +53,7 @@ int gd_pack_device_launch(const double *avals, const double *bvals, const int32_
                           int asize, int bsize, int nrows, uint64_t *acodes, uint64_t *bcodes, int32_t *rowpos,
                           unsigned *bad, hipStream_t s);
 int gd_fet_fast_windows_per_block();
+int gd_bounds_elems_per_block();
 int gd_fet_fast_init(hipStream_t s);
 int gd_fet_window_prepare(int64_t wtotal, int32_t *slow_list, unsigned *slow_count, hipStream_t s,
                           bool *force_general);
@@ -71,6 +72,27 @@ int gd_css_launch(int mp, int drosophila, int mds, const gd_chrom_dev *d_ch, int
                   hipStream_t s, hipEvent_t ev_perm);
 int gd_synth_launch(int chrom, int nsnp, int asize, int bsize, uint64_t seed, const double *freq_table,
                     double *avals, double *bvals, int32_t *apos, int32_t *bpos, hipStream_t s);
+
+/* general-path grid (gd_internal.h): resident capacity of the current device */
+int64_t gd_css_big_grid(int64_t wtotal, int mp) {
+  static std::atomic<int> cus{0};
+  int n = cus.load();
+  if (n == 0) {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) ==
+                                                 hipSuccess && v > 0)
+      n = v;
+    else
+      n = 256;
+    cus.store(n);
+  }
+  int64_t grid = (int64_t)n * (mp <= 256 ? 4 : 2);
+  if (const char *e = getenv("GD_CSS_BIG_GRID")) {
+    const long long g = atoll(e);
+    if (g > 0) grid = g;
+  }
+  return wtotal < grid ? wtotal : grid;
+}
 
 /* ------------------------------------------------------------------ errors */
 static thread_local std::string g_err;
@@ -488,7 +510,8 @@ static int fet_scan_locked(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, cons
                                          ctx->lut_hdr, ctx->lut, snp, sm)))
         return fail(st, "packed pass launch failed");
     } else {
-      const unsigned gxb = (unsigned)std::min<int64_t>((mx + 4095) / 4096, std::max(1, 8192 / nc));
+      const int64_t epb = gd_bounds_elems_per_block();
+      const unsigned gxb = (unsigned)std::min<int64_t>((mx + epb - 1) / epb, std::max(1, 8192 / nc));
       hipLaunchKernelGGL(k_bounds, dim3(gxb, nc, 2), dim3(256), 0, sm, d_ch + c0, apos, bpos, wsize, wstep, lo_a,
                          hi_a, lo_b, flags);
       const unsigned gxs = (unsigned)std::min<int64_t>((amax + 255) / 256, std::max(1, 8192 / nc));
@@ -820,7 +843,8 @@ static int css_scan_locked(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, cons
   } else {
     hipLaunchKernelGGL(k_popsize, dim3(nchrom), dim3(64), 0, s, d_ch, apos, bpos, flags);
     const int64_t mx = std::max(pl.max_alen, pl.max_blen) + 1;
-    const unsigned gx = (unsigned)std::min<int64_t>((mx + 4095) / 4096, std::max(1, 8192 / nchrom));
+    const int64_t epb = gd_bounds_elems_per_block();
+    const unsigned gx = (unsigned)std::min<int64_t>((mx + epb - 1) / epb, std::max(1, 8192 / nchrom));
     hipLaunchKernelGGL(k_bounds, dim3(gx, nchrom, 2), dim3(256), 0, s, d_ch, apos, bpos, wsize, wstep, lo_a,
                        hi_a, lo_b, flags);
   }
@@ -853,7 +877,7 @@ static int css_scan_locked(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, cons
   const int mp = gd_css_tier(mmax);
   if (mp == 0) return fail(GD_ERR_SIZE, "asize + bsize above the largest supported cohort (GD_CSS_BIG_MAX = 512)");
   /* the general path (m above the register tiers): one matrix slab per workgroup */
-  const int64_t slab_doubles = mp > GD_CSS_TIER_MAX ? gd_css_big_grid(pl.wtotal) * gd_css_big_slab_per_wg(mp) : 1;
+  const int64_t slab_doubles = mp > GD_CSS_TIER_MAX ? gd_css_big_grid(pl.wtotal, mp) * gd_css_big_slab_per_wg(mp) : 1;
   if (drosophila)
     for (int c = 0; c < nchrom; ++c) {
       const gd_chrom_dev &d = pl.h[c];

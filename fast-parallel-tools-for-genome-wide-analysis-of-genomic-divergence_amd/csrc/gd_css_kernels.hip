@@ -3125,7 +3125,7 @@ static int launch_big(int mp, const gd_chrom_dev *d_ch, int nchrom, const gd_css
                       const double *bvals, int64_t wtotal, int want_x, int force_literal, double *scores, double *p,
                       double *xbuf, uint8_t *status, unsigned *flags, double *slab, hipStream_t s) {
   const int ld = gd_css_big_ld(mp);
-  const int64_t per = gd_css_big_slab_per_wg(mp), grid = gd_css_big_grid(wtotal);
+  const int64_t per = gd_css_big_slab_per_wg(mp), grid = gd_css_big_grid(wtotal, mp);
   if (mp <= 256)
     hipLaunchKernelGGL(k_css_mds_big<256>, dim3((unsigned)grid), dim3(256), 0, s, d_ch, nchrom, d_pl, planes, lo_a,
                        hi_a, lo_b, avals, bvals, wtotal, want_x, force_literal, 2 * mp, scores, p, xbuf, status, flags,

@@ -1454,7 +1454,7 @@ int gd_css_perm_launch(int mp, const gd_chrom_dev *d_ch, int nchrom, const doubl
     case 128: return launch_perm<128>(d_ch, nchrom, xbuf, status, wtotal, treshold, runs, p, wq, s);
   }
   if (mp > GD_CSS_TIER_MAX && mp <= GD_CSS_BIG_MAX) {
-    const unsigned grid = (unsigned)gd_css_big_grid(wtotal);
+    const unsigned grid = (unsigned)gd_css_big_grid(wtotal, mp);
     const int64_t per = gd_css_big_slab_per_wg(mp);
     const int ld = gd_css_big_ld(mp);
     if (mp <= 256)

@@ -490,7 +490,7 @@ static int launch_smacof(const gd_chrom_dev *d_ch, int nchrom, const gd_css_plan
                          const double *bvals, int64_t wtotal, int mds, int want_x, int force_literal, int xstride,
                          double *scores, double *p, double *xbuf, uint8_t *status, unsigned *flags, hipStream_t s,
                          double *slab = nullptr, int mpb = 0) {
-  const int64_t grid = BIG ? gd_css_big_grid(wtotal) : wtotal;
+  const int64_t grid = BIG ? gd_css_big_grid(wtotal, mpb) : wtotal;
   hipLaunchKernelGGL((k_css_smacof<MP, FREQ, BIG>), dim3((unsigned)grid), dim3(64 * ((MP + 63) / 64)), 0, s, d_ch,
                      nchrom, d_pl, planes, lo_a, hi_a, lo_b, avals, bvals, wtotal, mds, want_x, force_literal,
                      xstride, scores, p, xbuf, status, flags, slab, BIG ? gd_css_big_slab_per_wg(mpb) : 0, mpb,

@@ -132,6 +132,7 @@ __global__ void __launch_bounds__(256) k_bounds(const gd_chrom_dev *ch, const in
 #ifndef KB_CH
 #define KB_CH 4 /* int4 chunks per lane and segment (loads in flight; 4: 0.326 ms per C2 bounds pass, 8: 0.312 (parity not yet run on the GPU), 2: 0.366) */
 #endif
+  static_assert(KB_CH >= 1 && 4 * KB_CH <= 32, "the boundary mask holds 4 KB_CH bits in a uint32_t");
   constexpr int KB_SEG = 256 * KB_CH;
 #ifndef KB_LDS
 #define KB_LDS 1
@@ -619,3 +620,7 @@ template __global__ void k_fet_window_general<256, true>(const gd_chrom_dev *, i
                                                          const double *, const double *, const uint64_t *,
                                                          const int *, const double *, double, double *, double *,
                                                          unsigned *, int32_t *, unsigned *, double *, int64_t);
+
+/* elements of one population's positions a k_bounds workgroup (4 waves) scans per pass:
+ * the launch sizes its grid from this, so it follows the KB_CH build switch */
+int gd_bounds_elems_per_block() { return 4 * 256 * KB_CH; }

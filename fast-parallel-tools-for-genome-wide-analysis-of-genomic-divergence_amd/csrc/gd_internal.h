@@ -40,10 +40,9 @@ typedef struct gd_chrom_dev {
 
 /* CSS cohort sizes (m = asize + bsize): register tiers up to GD_CSS_TIER_MAX; the general
  * path (k_css_mds_big, k_css_perm_big, k_css_smacof_big) above, up to GD_CSS_BIG_MAX, with
- * each workgroup's matrices in a global-memory slab of its own (L2 / Infinity-Cache resident) */
+ * each workgroup's matrices in a global-memory slab of its own */
 #define GD_CSS_TIER_MAX 128
 #define GD_CSS_BIG_MAX 512
-#define GD_CSS_BIG_GRID 1024 /* workgroups = slabs of the general-path kernels */
 /* leading dimension (doubles) of a general-path matrix: m rounded up to 128-byte columns */
 static inline int gd_css_big_ld(int m) { return (m + 15) & ~15; }
 /* doubles of one workgroup's slab: the m x ld matrix of the MDS / permutation kernels or
@@ -53,7 +52,12 @@ static inline int64_t gd_css_big_slab_per_wg(int m) {
   const int64_t sm = (int64_t)m * (m - 1) / 2 + 8 + ((int64_t)gd_css_big_ld(m) * m + 3) / 4 + 8;
   return (mds > sm ? mds : sm) + 32;
 }
-static inline int64_t gd_css_big_grid(int64_t wtotal) { return wtotal < GD_CSS_BIG_GRID ? wtotal : GD_CSS_BIG_GRID; }
+/* Workgroups (= slabs) of the general-path kernels for a batch of wtotal windows and tier
+ * mp: the device's resident capacity -- CUs x 4 workgroups of the 256-thread tier, x 2 of
+ * the 512-thread tier -- so every slab belongs to a running workgroup and the workgroups
+ * loop over windows (gd_api.hip).  GD_CSS_BIG_GRID=<n> overrides it (diagnostics: the
+ * tests force several windows per workgroup with it). */
+int64_t gd_css_big_grid(int64_t wtotal, int mp);
 
 /* CSS bit planes of one chromosome (word offsets into the plane buffer).  Pop A:
  * individual i's "== 3" plane at pa + 2i*wa, its "== -3" plane at pa + (2i+1)*wa,

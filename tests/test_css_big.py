@@ -79,3 +79,27 @@ def test_above_the_general_path_raises():
     av, bv, ap, bp, regend = synth.chromosome(240, 200, 300, 300)
     with pytest.raises(GdError):
         css.scan(av, bv, ap, bp, regend, serial=True)
+
+
+def test_general_path_several_windows_per_workgroup(oracle, opt, monkeypatch):
+    """The general-path kernels loop over windows with a slab per workgroup (grid = the
+    device's resident capacity); GD_CSS_BIG_GRID=3 forces each workgroup through many
+    windows, reusing its slab: MDS scores, permutation p (inside the oracle's tie bracket
+    on the device's coordinates) and SMACOF must still match the oracle."""
+    from gdscan import css, synth
+    monkeypatch.setenv("GD_CSS_BIG_GRID", "3")
+    a, b, nsnp, treshold, runs = 90, 80, 400, 10, 60
+    av, bv, ap, bp, regend = synth.chromosome(250, nsnp, a, b)
+    s, p, X = css.scan_coords(av, bv, ap, bp, regend, treshold=treshold, runs=runs, seed=17, serial=True)
+    s_ref, _ = oracle_css_scan(oracle, av, bv, ap, bp, regend, serial=True)
+    _cmp(s, s_ref, 20)
+    assert (s != 0).sum() > 3 * 6  # at least six windows per workgroup
+    bad = []
+    for w in np.flatnonzero(s != 0):
+        sc, p_lit, lo, hi, nt = _oracle_p(oracle, X[w], a, b, treshold, runs, 17, int(w))
+        if not lo <= p[w] <= hi:
+            bad.append((int(w), p[w], lo, hi))
+    assert not bad, bad[:10]
+    s1, _ = css.scan(av, bv, ap, bp, regend, runs=0, mds=1, seed=11, serial=True)
+    s1_ref, _ = oracle_scan_ex(opt, av, bv, ap, bp, regend, 0, 1, seed=11, serial=True)
+    assert _close_frac(s1, s1_ref, 1e-9) == 1.0

@@ -4,6 +4,7 @@
 #
 # usage: tools/gpu_session.sh OUT STEP [STEP ...]      (outputs under gpurun_out/OUT/)
 #   tests[=FILES]        pytest -m gpu over tests/ (or the listed test files, comma separated)
+#   testlib=TAG          the FET/compat GPU tests against tools/ab/TAG/libgdscan.so
 #   smoke                __graft_entry__.smoke()
 #   bench[=ARGS]         python bench.py ARGS (underscores in ARGS become spaces)
 #   fet[=TAG]            FET-only bench (20 steps), libgdscan.so of tools/ab/TAG if given
@@ -26,6 +27,9 @@ for S in "$@"; do
       F=tests; [ -n "$V" ] && F=${V//,/ }
       timeout -k 10 900 python -u -m pytest $F -m gpu -x -q --timeout 300 --timeout-method thread \
         > $O/$i.tests.log 2>&1 ;;
+    testlib)
+      GDSCAN_LIB=$(lib "$V") timeout -k 10 600 python -u -m pytest tests/test_fet_gpu.py tests/test_compat_gpu.py \
+        tests/test_packed.py -m gpu -x -q --timeout 300 --timeout-method thread > $O/$i.testlib$V.log 2>&1 ;;
     smoke)
       timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > $O/$i.smoke.log 2>&1 ;;
     bench)
