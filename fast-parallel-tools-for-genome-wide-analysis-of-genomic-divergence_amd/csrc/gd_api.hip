@@ -875,7 +875,7 @@ static int css_scan_locked(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, cons
     max_words = std::max(max_words, std::max(wa * d.asize, wb * d.bsize));
   }
   const int mp = gd_css_tier(mmax);
-  if (mp == 0) return fail(GD_ERR_SIZE, "asize + bsize above the largest supported cohort (GD_CSS_BIG_MAX = 512)");
+  if (mp == 0) return fail(GD_ERR_SIZE, "asize + bsize above the largest supported cohort (GD_CSS_BIG_MAX = 1024)");
   /* the general path (m above the register tiers): one matrix slab per workgroup */
   const int64_t slab_doubles = mp > GD_CSS_TIER_MAX ? gd_css_big_grid(pl.wtotal, mp) * gd_css_big_slab_per_wg(mp) : 1;
   if (drosophila)

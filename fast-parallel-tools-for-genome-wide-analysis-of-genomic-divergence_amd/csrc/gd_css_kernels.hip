@@ -283,9 +283,11 @@ __device__ __forceinline__ double css_score(const int *tracks, int a, int b, Dis
   constexpr int NT = 64 * NW;
   const int t = threadIdx.x, ab = a * b, m = a + b;
   const float invb = 1.0f / (float)b;
+  const gd_randint db = gd_randint_make((uint32_t)(b > 1 ? b : 2)); /* exact q / b above 2^14 pairs */
   double bet = 0, win = 0;
   for (int q = t; q < ab; q += NT) {
-    const int ii = (int)(((float)q + 0.5f) * invb); /* exact for q < 2^14 */
+    const int ii = ab <= (1 << 14) ? (int)(((float)q + 0.5f) * invb) /* exact for q < 2^14 */
+                                   : (b == 1 ? q : (int)(__umulhi((uint32_t)q, db.magic) >> db.shift));
     const int jj = q - ii * b;
     bet += dist(tracks[ii], tracks[a + jj]);
   }
@@ -2772,20 +2774,23 @@ __global__ void __launch_bounds__(64, CSS_P40_WAVES)
 /* same algorithm as k_css_mds -- compare_all by popcounts (literal predicate for */
 /* irregular windows), fill_averages, double centering, Householder (dsytd2,      */
 /* lower), bisection for the top two eigenvalues, inverse iteration, back-        */
-/* transformation, X, css -- with thread i owning row i and the matrix in a       */
-/* global-memory slab of the workgroup's own, column-major (element (i, j) at     */
-/* j ld + i): every sweep over a column touches one contiguous 8 m-byte run, so a */
-/* wave's loads coalesce, and the slab (m ld doubles) stays cache-resident.  The  */
-/* workgroups loop over windows (grid = number of slabs).                         */
+/* transformation, X, css -- with thread t owning rows t, t + NT, .. (R rows,      */
+/* NT = MP / R threads) and the matrix in a global-memory slab of the workgroup's */
+/* own, column-major (element (i, j) at j ld + i): every sweep over a column      */
+/* touches one contiguous 8 m-byte run, so a wave's loads coalesce.  The          */
+/* workgroups loop over windows (grid = the device's resident capacity,           */
+/* gd_css_big_grid).  Above 512 individuals (R = 2) the inverse-iteration factors */
+/* live in the slab behind the matrix instead of LDS.                             */
 /* ------------------------------------------------------------------------ */
-template <int MP>
-__global__ void __launch_bounds__(MP)
+template <int MP, int R>
+__global__ void __launch_bounds__(MP / R)
     k_css_mds_big(const gd_chrom_dev *ch, int nchrom, const gd_css_planes *pl, const uint32_t *planes,
                   const int32_t *lo_a_, const int32_t *hi_a_, const int32_t *lo_b_, const double *avals,
                   const double *bvals, int64_t wtotal, int want_x, int force_literal, int xstride, double *scores,
                   double *pvals, double *xbuf, uint8_t *status, unsigned *flags, double *slab, int64_t slab_per_wg,
                   int ld) {
-  constexpr int NT = MP, NW = MP / 64;
+  constexpr int NT = MP / R, NW = NT / 64;
+  constexpr bool LUG = R > 1; /* inverse-iteration factors in the slab (LDS budget) */
   __shared__ double s_row[MP + 2];
   __shared__ double s_v[MP], s_w[MP];
   __shared__ __attribute__((aligned(16))) double s_d[MP + 4];
@@ -2793,17 +2798,23 @@ __global__ void __launch_bounds__(MP)
   __shared__ double s_e[MP], s_tau[MP];
   __shared__ uint64_t s_mask[2 * MP];
   __shared__ double s_y[2][MP];
-  __shared__ double s_lu[2][3][MP];
-  __shared__ uint8_t s_piv[2][MP];
+  __shared__ double s_lu_l[2][3][LUG ? 1 : MP];
+  __shared__ uint8_t s_piv_l[2][LUG ? 1 : MP];
   __shared__ double s_x[2 * MP];
   __shared__ int s_tr[MP];
   __shared__ double s_lam[2];
   __shared__ double s_red[2 * (2 * NW + 2)];
 
-  const int tid = threadIdx.x, i = tid;
+  const int tid = threadIdx.x;
   double *A = slab + (int64_t)blockIdx.x * slab_per_wg;
+  static_assert(!LUG || MP == 1024, "GD_CSS_BIG_LU_DOUBLES is sized for the 1024 tier");
+  double *lug = A + slab_per_wg - GD_CSS_BIG_LU_DOUBLES; /* the slab's tail (gd_css_big_slab_per_wg) */
+  double(*s_lu)[3][MP] = LUG ? reinterpret_cast<double(*)[3][MP]>(lug)
+                             : reinterpret_cast<double(*)[3][MP]>(&s_lu_l[0][0][0]);
+  uint8_t(*s_piv)[MP] = LUG ? reinterpret_cast<uint8_t(*)[MP]>(lug + 6 * MP)
+                            : reinterpret_cast<uint8_t(*)[MP]>(&s_piv_l[0][0]);
   auto at = [&](int r, int c) -> double & { return A[(int64_t)c * ld + r]; };
-  s_tr[tid] = tid;
+  for (int t = tid; t < MP; t += NT) s_tr[t] = t;
 
   for (int64_t w = blockIdx.x; w < wtotal; w += gridDim.x) {
     const int c = chrom_of(ch, nchrom, w);
@@ -2821,7 +2832,6 @@ __global__ void __launch_bounds__(MP)
       if (tid == 0) atomicOr(flags, GD_FLAG_BAD_SIZE);
       continue;
     }
-    const bool row = i < m;
     const gd_css_planes P = pl[c];
     const uint32_t *pa = planes + P.pa, *pb = planes + P.pb;
     const int64_t ra = la / a, rb = lb / b;
@@ -2847,37 +2857,50 @@ __global__ void __launch_bounds__(MP)
         const int nb = min(64, npos - 64 * k);
         const uint64_t tail = nb == 64 ? ~0ull : ((1ull << nb) - 1);
         __syncthreads();
-        if (row) {
-          const uint32_t *base = i < a ? pa + (int64_t)(2 * i) * P.wa : pb + (int64_t)(2 * (i - a)) * P.wb;
-          const int64_t nw = i < a ? P.wa : P.wb;
-          const int64_t r = (i < a ? ra : rb) + 64 * k;
-          s_mask[2 * i] = plane_bits64(base, r) & tail;
-          s_mask[2 * i + 1] = plane_bits64(base + nw, r) & tail;
+#pragma unroll
+        for (int rr = 0; rr < R; ++rr) {
+          const int i = tid + rr * NT;
+          if (i < m) {
+            const uint32_t *base = i < a ? pa + (int64_t)(2 * i) * P.wa : pb + (int64_t)(2 * (i - a)) * P.wb;
+            const int64_t nw = i < a ? P.wa : P.wb;
+            const int64_t r = (i < a ? ra : rb) + 64 * k;
+            s_mask[2 * i] = plane_bits64(base, r) & tail;
+            s_mask[2 * i + 1] = plane_bits64(base + nw, r) & tail;
+          }
         }
         __syncthreads();
-        if (row) {
-          const uint64_t Pi = s_mask[2 * i], Ni = s_mask[2 * i + 1];
-          for (int j = 0; j < m; ++j) {
-            const double cnt = (double)(__popcll(Pi & s_mask[2 * j + 1]) + __popcll(Ni & s_mask[2 * j]));
-            at(i, j) = k == 0 ? cnt : at(i, j) + cnt;
+#pragma unroll
+        for (int rr = 0; rr < R; ++rr) {
+          const int i = tid + rr * NT;
+          if (i < m) {
+            const uint64_t Pi = s_mask[2 * i], Ni = s_mask[2 * i + 1];
+            for (int j = 0; j < m; ++j) {
+              const double cnt = (double)(__popcll(Pi & s_mask[2 * j + 1]) + __popcll(Ni & s_mask[2 * j]));
+              at(i, j) = k == 0 ? cnt : at(i, j) + cnt;
+            }
           }
         }
       }
-    } else if (row) {
+    } else {
       const double *av = avals + d.a_off + la, *bv = bvals + d.b_off + lb;
       auto val = [&](int r, int k) { return r < a ? av[(int64_t)k * a + r] : bv[(int64_t)k * b + (r - a)]; };
-      for (int j = 0; j < m; ++j) {
-        int cnt = 0;
-        /* the reference casts the row element of the larger index within a population and
-         * the A element across populations (css.c:281-326); the diagonal never counts */
-        const bool cast_i = ((i < a) == (j < a)) ? (i > j) : (i < a);
-        if (j != i)
-          for (int k = 0; k < npos; ++k) {
-            const double vi = val(i, k), vj = val(j, k);
-            const double prod = cast_i ? x86_int(vi) * vj : x86_int(vj) * vi;
-            cnt += prod == -9.0;
+#pragma unroll 1
+      for (int rr = 0; rr < R; ++rr) {
+        const int i = tid + rr * NT;
+        if (i < m)
+          for (int j = 0; j < m; ++j) {
+            int cnt = 0;
+            /* the reference casts the row element of the larger index within a population and
+             * the A element across populations (css.c:281-326); the diagonal never counts */
+            const bool cast_i = ((i < a) == (j < a)) ? (i > j) : (i < a);
+            if (j != i)
+              for (int k = 0; k < npos; ++k) {
+                const double vi = val(i, k), vj = val(j, k);
+                const double prod = cast_i ? x86_int(vi) * vj : x86_int(vj) * vi;
+                cnt += prod == -9.0;
+              }
+            at(i, j) = (double)cnt;
           }
-        at(i, j) = (double)cnt;
       }
     }
 
@@ -2885,39 +2908,53 @@ __global__ void __launch_bounds__(MP)
     double zero_tol;
     {
       double unv = 0.0, sum = 0.0;
-      if (row)
-        for (int j = 0; j < m; ++j) {
-          const double x = at(i, j);
-          if (x < 0.00001)
-            unv += 1.0;
-          else
-            sum += x;
-        }
+#pragma unroll
+      for (int rr = 0; rr < R; ++rr) {
+        const int i = tid + rr * NT;
+        if (i < m)
+          for (int j = 0; j < m; ++j) {
+            const double x = at(i, j);
+            if (x < 0.00001)
+              unv += 1.0;
+            else
+              sum += x;
+          }
+      }
       block_sum2<NW>(unv, sum, s_red); /* sums of integers: exact in any order */
       const int tot = m * m;
       if ((int)unv > tot / 2) continue; /* discarded window: outputs untouched */
       const double avg = sum / tot;
       /* B = -1/2 Z (D o D) Z by double centering, as k_css_mds */
-      double rs = 0.0;
-      if (row)
-        for (int j = 0; j < m; ++j) {
-          double x = at(i, j);
-          x = fma(avg, 1.0 - fmin(x, 1.0), x);
-          x = x * x;
-          at(i, j) = x;
-          rs += x;
-        }
-      const double ri = row ? rs / m : 0.0;
-      s_v[i] = ri;
-      const double g = block_sum<NW>(ri, s_red) / m;
+      double ri[R], rsum = 0.0;
+#pragma unroll
+      for (int rr = 0; rr < R; ++rr) {
+        const int i = tid + rr * NT;
+        double rs = 0.0;
+        if (i < m)
+          for (int j = 0; j < m; ++j) {
+            double x = at(i, j);
+            x = fma(avg, 1.0 - fmin(x, 1.0), x);
+            x = x * x;
+            at(i, j) = x;
+            rs += x;
+          }
+        ri[rr] = i < m ? rs / m : 0.0;
+        if (i < MP) s_v[i] = ri[rr];
+        rsum += ri[rr];
+      }
+      const double g = block_sum<NW>(rsum, s_red) / m;
       __syncthreads();
       double f2 = 0.0;
-      if (row)
-        for (int j = 0; j < m; ++j) {
-          const double x = -0.5 * ((at(i, j) - (ri + s_v[j])) + g);
-          at(i, j) = x;
-          f2 = fma(x, x, f2);
-        }
+#pragma unroll
+      for (int rr = 0; rr < R; ++rr) {
+        const int i = tid + rr * NT;
+        if (i < m)
+          for (int j = 0; j < m; ++j) {
+            const double x = -0.5 * ((at(i, j) - (ri[rr] + s_v[j])) + g);
+            at(i, j) = x;
+            f2 = fma(x, x, f2);
+          }
+      }
       zero_tol = 64.0 * m * DBL_EPSILON * sqrt(block_sum<NW>(f2, s_red));
     }
 
@@ -2926,31 +2963,44 @@ __global__ void __launch_bounds__(MP)
     for (int k = 0; k < m; ++k) {
       __syncthreads();
       /* row k right of the diagonal (zeros at j <= k) and d_k; A(k, j) as lane k holds it */
-      if (row) s_row[i] = i > k ? at(k, i) : 0.0;
-      if (i == k) s_d[k] = at(k, k);
+#pragma unroll
+      for (int rr = 0; rr < R; ++rr) {
+        const int i = tid + rr * NT;
+        if (i < m) s_row[i] = i > k ? at(k, i) : 0.0;
+        if (i == k) s_d[k] = at(k, k);
+      }
       __syncthreads();
       if (k >= m - 2) {
         if (tid == 0 && k == m - 2) s_e[k] = s_row[k + 1];
         continue;
       }
-      const double xi = (i > k + 1 && row) ? s_row[i] : 0.0;
       const double alpha = s_row[k + 1];
-      double praw = 0.0, ak1 = 0.0;
-      if (i > k && row) {
-        double p0 = 0.0, p1 = 0.0;
-        int j = k + 1;
-        for (; j + 1 < m; j += 2) {
-          p0 = fma(at(i, j), s_row[j], p0);
-          p1 = fma(at(i, j + 1), s_row[j + 1], p1);
+      double xi[R], praw[R], ak1[R];
+      double sigma = 0.0, q = 0.0;
+#pragma unroll
+      for (int rr = 0; rr < R; ++rr) {
+        const int i = tid + rr * NT;
+        const bool row = i < m;
+        xi[rr] = (i > k + 1 && row) ? s_row[i] : 0.0;
+        praw[rr] = 0.0;
+        ak1[rr] = 0.0;
+        if (i > k && row) {
+          double p0 = 0.0, p1 = 0.0;
+          int j = k + 1;
+          for (; j + 1 < m; j += 2) {
+            p0 = fma(at(i, j), s_row[j], p0);
+            p1 = fma(at(i, j + 1), s_row[j + 1], p1);
+          }
+          if (j < m) p0 = fma(at(i, j), s_row[j], p0);
+          praw[rr] = p0 + p1;
+          ak1[rr] = at(i, k + 1);
         }
-        if (j < m) p0 = fma(at(i, j), s_row[j], p0);
-        praw = p0 + p1;
-        ak1 = at(i, k + 1);
-      }
-      double sigma = xi * xi, q = (i > k && row) ? s_row[i] * praw : 0.0;
-      if (i == k + 1) {
-        s_red[2 * NW] = praw;
-        s_red[2 * NW + 1] = ak1;
+        sigma = fma(xi[rr], xi[rr], sigma);
+        if (i > k && row) q = fma(s_row[i], praw[rr], q);
+        if (i == k + 1) {
+          s_red[2 * NW] = praw[rr];
+          s_red[2 * NW + 1] = ak1[rr];
+        }
       }
       block_sum2<NW>(sigma, q, s_red);
       const double pr1 = s_red[2 * NW], a11 = s_red[2 * NW + 1];
@@ -2962,20 +3012,32 @@ __global__ void __launch_bounds__(MP)
         scale = beta * r;
       }
       /* v = scale (x - beta e_{k+1}), v_{k+1} = 1;  p = tau A v;  w = p + K v */
-      const double vi = (i == k + 1) ? 1.0 : xi * scale;
-      const double pi = (i > k && row) ? (tau * scale) * fma(-beta, ak1, praw) : 0.0;
       const double K = -0.5 * tau * (tau * scale * scale) * fma(beta, fma(beta, a11, -2.0 * pr1), q);
-      const double wi = fma(K, vi, pi);
+      double vi[R], wi[R];
+#pragma unroll
+      for (int rr = 0; rr < R; ++rr) {
+        const int i = tid + rr * NT;
+        const bool row = i < m;
+        vi[rr] = (i == k + 1) ? 1.0 : xi[rr] * scale;
+        const double pi = (i > k && row) ? (tau * scale) * fma(-beta, ak1[rr], praw[rr]) : 0.0;
+        wi[rr] = fma(K, vi[rr], pi);
+        if (i < MP) {
+          s_v[i] = vi[rr];
+          s_w[i] = wi[rr];
+        }
+      }
       if (tid == 0) {
         s_e[k] = beta;
         s_tau[k] = tau;
       }
-      s_v[i] = vi;
-      s_w[i] = wi;
       __syncthreads();
-      if (i > k && row)
-        for (int j = k + 1; j < m; ++j) at(i, j) = fma(-vi, s_w[j], fma(-wi, s_v[j], at(i, j)));
-      if (row) at(i, k) = vi; /* stash v_k in the dead column k */
+#pragma unroll
+      for (int rr = 0; rr < R; ++rr) {
+        const int i = tid + rr * NT;
+        if (i > k && i < m)
+          for (int j = k + 1; j < m; ++j) at(i, j) = fma(-vi[rr], s_w[j], fma(-wi[rr], s_v[j], at(i, j)));
+        if (i < m) at(i, k) = vi[rr]; /* stash v_k in the dead column k */
+      }
     }
     __syncthreads();
 
@@ -2983,10 +3045,14 @@ __global__ void __launch_bounds__(MP)
     double glo, ghi;
     {
       double lo = DBL_MAX, hi = -DBL_MAX;
-      if (row) {
-        const double r = (i > 0 ? fabs(s_e[i - 1]) : 0.0) + (i < m - 1 ? fabs(s_e[i]) : 0.0);
-        lo = s_d[i] - r;
-        hi = s_d[i] + r;
+#pragma unroll
+      for (int rr = 0; rr < R; ++rr) {
+        const int i = tid + rr * NT;
+        if (i < m) {
+          const double r = (i > 0 ? fabs(s_e[i - 1]) : 0.0) + (i < m - 1 ? fabs(s_e[i]) : 0.0);
+          lo = fmin(lo, s_d[i] - r);
+          hi = fmax(hi, s_d[i] + r);
+        }
       }
       for (int t = tid; t < MP + 4; t += NT) s_e2[t] = (t >= 1 && t < m) ? s_e[t - 1] * s_e[t - 1] : 0.0;
       glo = block_reduce<NW, OpMin>(lo, s_red);
@@ -3005,53 +3071,88 @@ __global__ void __launch_bounds__(MP)
     /* ---- eigenvectors of T: two inverse-iteration solves, orthogonalised */
     if (tid < 2) invit_factor<MP>(m, tid, s_d, s_e, s_lam, s_lu, s_x, s_piv, s_y);
     __syncthreads();
-    if (row) {
+    {
       const double tiny = DBL_EPSILON * fmax(fmax(fabs(glo), fabs(ghi)), DBL_MIN);
 #pragma unroll
-      for (int e = 0; e < 2; ++e) {
-        const double u0 = s_lu[e][0][i];
-        s_lu[e][0][i] = fast_rcp(u0 == 0.0 ? tiny : u0);
+      for (int rr = 0; rr < R; ++rr) {
+        const int i = tid + rr * NT;
+        if (i < m)
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            const double u0 = s_lu[e][0][i];
+            s_lu[e][0][i] = fast_rcp(u0 == 0.0 ? tiny : u0);
+          }
       }
     }
-    double y1 = 0.0, y2 = 0.0;
+    double y1[R], y2[R];
+#pragma unroll
+    for (int rr = 0; rr < R; ++rr) y1[rr] = y2[rr] = 0.0;
     for (int itn = 0; itn < 2; ++itn) {
+      __threadfence_block();
       __syncthreads();
       if (tid < 2) invit_solve<MP>(m, tid, s_lu, s_x, s_piv, s_y);
       __syncthreads();
-      y1 = row ? s_y[0][i] : 0.0;
-      y2 = row ? s_y[1][i] : 0.0;
-      double n1 = y1 * y1, n2 = y2 * y2;
+      double n1 = 0.0, n2 = 0.0;
+#pragma unroll
+      for (int rr = 0; rr < R; ++rr) {
+        const int i = tid + rr * NT;
+        y1[rr] = i < m ? s_y[0][i] : 0.0;
+        y2[rr] = i < m ? s_y[1][i] : 0.0;
+        n1 = fma(y1[rr], y1[rr], n1);
+        n2 = fma(y2[rr], y2[rr], n2);
+      }
       block_sum2<NW>(n1, n2, s_red);
-      y1 *= 1.0 / sqrt(n1);
-      y2 *= 1.0 / sqrt(n2);
+      const double s1 = 1.0 / sqrt(n1), s2 = 1.0 / sqrt(n2);
       __syncthreads();
-      if (itn == 0 && row) {
-        s_y[0][i] = y1;
-        s_y[1][i] = y2;
+#pragma unroll
+      for (int rr = 0; rr < R; ++rr) {
+        const int i = tid + rr * NT;
+        y1[rr] *= s1;
+        y2[rr] *= s2;
+        if (itn == 0 && i < m) {
+          s_y[0][i] = y1[rr];
+          s_y[1][i] = y2[rr];
+        }
       }
     }
     {
-      double dt = y1 * y2, zero = 0.0;
+      double dt = 0.0, zero = 0.0;
+#pragma unroll
+      for (int rr = 0; rr < R; ++rr) dt = fma(y1[rr], y2[rr], dt);
       block_sum2<NW>(dt, zero, s_red);
-      y2 = fma(-dt, y1, y2);
-      double n2 = y2 * y2;
+      double n2 = 0.0;
+#pragma unroll
+      for (int rr = 0; rr < R; ++rr) {
+        y2[rr] = fma(-dt, y1[rr], y2[rr]);
+        n2 = fma(y2[rr], y2[rr], n2);
+      }
       zero = 0.0;
       block_sum2<NW>(n2, zero, s_red);
-      y2 *= 1.0 / sqrt(n2);
+      const double s2 = 1.0 / sqrt(n2);
+#pragma unroll
+      for (int rr = 0; rr < R; ++rr) y2[rr] *= s2;
     }
     {
       __syncthreads();
-      if (row) {
-        s_y[0][i] = y1;
-        s_y[1][i] = y2;
+#pragma unroll
+      for (int rr = 0; rr < R; ++rr) {
+        const int i = tid + rr * NT;
+        if (i < m) {
+          s_y[0][i] = y1[rr];
+          s_y[1][i] = y2[rr];
+        }
       }
       __syncthreads();
       double t1 = 0.0, t2 = 0.0;
-      if (row) {
-        const double el = i > 0 ? s_e[i - 1] : 0.0, er = i + 1 < m ? s_e[i] : 0.0;
-        const int il = i > 0 ? i - 1 : 0, ir = i + 1 < m ? i + 1 : i;
-        t1 = y1 * (s_d[i] * y1 + el * s_y[0][il] + er * s_y[0][ir]);
-        t2 = y2 * (s_d[i] * y2 + el * s_y[1][il] + er * s_y[1][ir]);
+#pragma unroll
+      for (int rr = 0; rr < R; ++rr) {
+        const int i = tid + rr * NT;
+        if (i < m) {
+          const double el = i > 0 ? s_e[i - 1] : 0.0, er = i + 1 < m ? s_e[i] : 0.0;
+          const int il = i > 0 ? i - 1 : 0, ir = i + 1 < m ? i + 1 : i;
+          t1 += y1[rr] * (s_d[i] * y1[rr] + el * s_y[0][il] + er * s_y[0][ir]);
+          t2 += y2[rr] * (s_d[i] * y2[rr] + el * s_y[1][il] + er * s_y[1][ir]);
+        }
       }
       block_sum2<NW>(t1, t2, s_red);
       if (tid == 0) {
@@ -3063,21 +3164,34 @@ __global__ void __launch_bounds__(MP)
 
     /* ---- back-transformation y <- H_0 H_1 ... H_{m-3} y (v_k in column k) */
     for (int k = m - 3; k >= 0; --k) {
-      const double vk = row ? at(i, k) : 0.0;
+      double vk[R], d1 = 0.0, d2 = 0.0;
+#pragma unroll
+      for (int rr = 0; rr < R; ++rr) {
+        const int i = tid + rr * NT;
+        vk[rr] = i < m ? at(i, k) : 0.0;
+        d1 = fma(vk[rr], y1[rr], d1);
+        d2 = fma(vk[rr], y2[rr], d2);
+      }
       const double t = s_tau[k];
-      double d1 = vk * y1, d2 = vk * y2;
       block_sum2<NW>(d1, d2, s_red);
-      y1 = fma(-(t * d1), vk, y1);
-      y2 = fma(-(t * d2), vk, y2);
+#pragma unroll
+      for (int rr = 0; rr < R; ++rr) {
+        y1[rr] = fma(-(t * d1), vk[rr], y1[rr]);
+        y2[rr] = fma(-(t * d2), vk[rr], y2[rr]);
+      }
     }
 
     /* ---- X = Q sqrt(L) (css.c:545-556), then calc_dist + css on identity groups */
     {
       const double L1 = sqrt(s_lam[0]), L2 = sqrt(s_lam[1]);
       __syncthreads();
-      if (row) {
-        s_x[2 * i] = y1 * L1 + y2 * 0.0;
-        s_x[2 * i + 1] = y1 * 0.0 + y2 * L2;
+#pragma unroll
+      for (int rr = 0; rr < R; ++rr) {
+        const int i = tid + rr * NT;
+        if (i < m) {
+          s_x[2 * i] = y1[rr] * L1 + y2[rr] * 0.0;
+          s_x[2 * i + 1] = y1[rr] * 0.0 + y2[rr] * L2;
+        }
       }
       __syncthreads();
     }
@@ -3126,14 +3240,17 @@ static int launch_big(int mp, const gd_chrom_dev *d_ch, int nchrom, const gd_css
                       double *xbuf, uint8_t *status, unsigned *flags, double *slab, hipStream_t s) {
   const int ld = gd_css_big_ld(mp);
   const int64_t per = gd_css_big_slab_per_wg(mp), grid = gd_css_big_grid(wtotal, mp);
+#define CSS_BIG(T, RR)                                                                                             \
+  hipLaunchKernelGGL((k_css_mds_big<T, RR>), dim3((unsigned)grid), dim3(T / RR), 0, s, d_ch, nchrom, d_pl, planes, \
+                     lo_a, hi_a, lo_b, avals, bvals, wtotal, want_x, force_literal, 2 * mp, scores, p, xbuf, status,  \
+                     flags, slab, per, ld)
   if (mp <= 256)
-    hipLaunchKernelGGL(k_css_mds_big<256>, dim3((unsigned)grid), dim3(256), 0, s, d_ch, nchrom, d_pl, planes, lo_a,
-                       hi_a, lo_b, avals, bvals, wtotal, want_x, force_literal, 2 * mp, scores, p, xbuf, status, flags,
-                       slab, per, ld);
+    CSS_BIG(256, 1);
+  else if (mp <= 512)
+    CSS_BIG(512, 1);
   else
-    hipLaunchKernelGGL(k_css_mds_big<512>, dim3((unsigned)grid), dim3(512), 0, s, d_ch, nchrom, d_pl, planes, lo_a,
-                       hi_a, lo_b, avals, bvals, wtotal, want_x, force_literal, 2 * mp, scores, p, xbuf, status, flags,
-                       slab, per, ld);
+    CSS_BIG(1024, 2);
+#undef CSS_BIG
   return hipGetLastError() == hipSuccess ? GD_OK : GD_ERR_HIP;
 }
 

@@ -1207,10 +1207,13 @@ __global__ void __launch_bounds__(PermShape<MP>::NT) PERM_WPE
 /* observed score is the same function of the identity tracks.                    */
 /* ------------------------------------------------------------------------ */
 namespace {
-constexpr int PB_P = 64; /* permutations per pass */
+/* permutations per pass: 64, 32 at the 1024 tier (its byte-pair matrix is MP x P u16) */
+template <int MP>
+constexpr int pb_p() { return MP > 512 ? 32 : 64; }
 
 /* Fisher-Yates of random_shuffle (css.c:700-706) on column `col` (stride PB_P), draws
  * from state x without rejection; true if a draw would have been rejected */
+template <int PB_P>
 __device__ __forceinline__ bool fy_big_fast(uint16_t *col, uint64_t x, int m, const uint32_t *mag) {
   bool rej = false;
   uint64_t y = x << 16;
@@ -1229,6 +1232,7 @@ __device__ __forceinline__ bool fy_big_fast(uint16_t *col, uint64_t x, int m, co
 }
 
 /* the same with random_int_nrand48's redraw loop (css.c:675-690) */
+template <int PB_P>
 __device__ __forceinline__ void fy_big_exact(uint16_t *col, uint64_t x, int m, const uint32_t *mag) {
   for (int s = 0; s < m - 1; ++s) {
     const int n = __builtin_amdgcn_readfirstlane(m - s);
@@ -1284,7 +1288,7 @@ __global__ void __launch_bounds__(256)
     k_css_perm_big(const gd_chrom_dev *ch, int nchrom, const double *xbuf, int xstride, const uint8_t *status,
                    int64_t wtotal, int treshold, int runs, double *pvals, unsigned *wq, double *slab,
                    int64_t slab_per_wg, int ld) {
-  constexpr int NT = 256, P = PB_P;
+  constexpr int NT = 256, P = pb_p<MP>();
   __shared__ uint16_t s_sig[MP * P]; /* element k of column q at k P + q */
   __shared__ uint16_t s_F[2][MP];    /* the carried tracks, double-buffered while composing */
   __shared__ double s_X[2 * MP];
@@ -1340,9 +1344,9 @@ __global__ void __launch_bounds__(256)
       /* 1. draws: wave 0, lane q -> sigma_q in column q */
       uint16_t *col = s_sig + lane;
       bool rej = false;
-      if (wave == 0) {
+      if (wave == 0 && lane < P) {
         for (int k = 0; k < m; ++k) col[k * P] = (uint16_t)k;
-        rej = fy_big_fast(col, gd_affine_apply(Jq, base), m, s_mag);
+        rej = fy_big_fast<P>(col, gd_affine_apply(Jq, base), m, s_mag);
       }
       if (__syncthreads_or(rej)) {
         if (tid == 0) {
@@ -1358,9 +1362,9 @@ __global__ void __launch_bounds__(256)
           s_st[P] = y;
         }
         __syncthreads();
-        if (wave == 0) {
+        if (wave == 0 && lane < P) {
           for (int k = 0; k < m; ++k) col[k * P] = (uint16_t)k;
-          fy_big_exact(col, s_st[lane], m, s_mag);
+          fy_big_exact<P>(col, s_st[lane], m, s_mag);
         }
         base = s_st[P];
       } else {
@@ -1460,9 +1464,12 @@ int gd_css_perm_launch(int mp, const gd_chrom_dev *d_ch, int nchrom, const doubl
     if (mp <= 256)
       hipLaunchKernelGGL(k_css_perm_big<256>, dim3(grid), dim3(256), 0, s, d_ch, nchrom, xbuf, 2 * mp, status, wtotal,
                          treshold, runs, p, wq, slab, per, ld);
-    else
+    else if (mp <= 512)
       hipLaunchKernelGGL(k_css_perm_big<512>, dim3(grid), dim3(256), 0, s, d_ch, nchrom, xbuf, 2 * mp, status, wtotal,
                          treshold, runs, p, wq, slab, per, ld);
+    else
+      hipLaunchKernelGGL(k_css_perm_big<1024>, dim3(grid), dim3(256), 0, s, d_ch, nchrom, xbuf, 2 * mp, status,
+                         wtotal, treshold, runs, p, wq, slab, per, ld);
     return hipGetLastError() == hipSuccess ? GD_OK : GD_ERR_HIP;
   }
   return GD_ERR_SIZE;

@@ -42,7 +42,9 @@ typedef struct gd_chrom_dev {
  * path (k_css_mds_big, k_css_perm_big, k_css_smacof_big) above, up to GD_CSS_BIG_MAX, with
  * each workgroup's matrices in a global-memory slab of its own */
 #define GD_CSS_TIER_MAX 128
-#define GD_CSS_BIG_MAX 512
+#define GD_CSS_BIG_MAX 1024
+/* doubles at the end of a 1024-tier slab for the inverse-iteration factors (LDS budget) */
+#define GD_CSS_BIG_LU_DOUBLES (6 * 1024 + 2 * 1024 / 8 + 8)
 /* leading dimension (doubles) of a general-path matrix: m rounded up to 128-byte columns */
 static inline int gd_css_big_ld(int m) { return (m + 15) & ~15; }
 /* doubles of one workgroup's slab: the m x ld matrix of the MDS / permutation kernels or
@@ -50,11 +52,11 @@ static inline int gd_css_big_ld(int m) { return (m + 15) & ~15; }
 static inline int64_t gd_css_big_slab_per_wg(int m) {
   const int64_t mds = (int64_t)gd_css_big_ld(m) * m;
   const int64_t sm = (int64_t)m * (m - 1) / 2 + 8 + ((int64_t)gd_css_big_ld(m) * m + 3) / 4 + 8;
-  return (mds > sm ? mds : sm) + 32;
+  return (mds > sm ? mds : sm) + 32 + (m > 512 ? GD_CSS_BIG_LU_DOUBLES : 0);
 }
 /* Workgroups (= slabs) of the general-path kernels for a batch of wtotal windows and tier
  * mp: the device's resident capacity -- CUs x 4 workgroups of the 256-thread tier, x 2 of
- * the 512-thread tier -- so every slab belongs to a running workgroup and the workgroups
+ * the 512-thread tiers (512 and 1024 individuals) -- so every slab belongs to a running workgroup and the workgroups
  * loop over windows (gd_api.hip).  GD_CSS_BIG_GRID=<n> overrides it (diagnostics: the
  * tests force several windows per workgroup with it). */
 int64_t gd_css_big_grid(int64_t wtotal, int mp);

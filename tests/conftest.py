@@ -171,3 +171,43 @@ def load_scan_fixture(name):
 
 
 SCAN_FIXTURES = ["10x10", "20x20", "7x13_w1000", "small_serial", "perc50"]
+
+
+def window_slices(ap, bp, regend, a, b, wsize=2500, wstep=500, serial=False):
+    """{window: (A element offset, B element offset, rows)} of the computed-window set, as
+    the oracle's scans slice it (slide_right, comparative.c:49-71; sorted positions)."""
+    lib = ctypes.CDLL(str(ORACLE_LIB))
+    lib.orc_serial_window_end.argtypes = lib.orc_threaded_window_end.argtypes = [ctypes.c_int] * 3
+    end = (lib.orc_serial_window_end if serial else lib.orc_threaded_window_end)(regend, wsize, wstep)
+    out = {}
+    for w in range(end):
+        start, stop = w * wstep, w * wstep + wsize
+        la0, la1 = int(np.searchsorted(ap, start, "left")), int(np.searchsorted(ap, stop, "right"))
+        npos = (la1 - la0) // a
+        if npos > 0:
+            out[w] = (la0, int(np.searchsorted(bp, start, "left")), npos)
+    return out
+
+
+def assert_p_mismatches_are_ties(oracle, av, bv, ap, bp, regend, a, b, p_dev, p_ref, treshold, runs, seed,
+                                 serial=False, mds=0):
+    """Every window whose permutation p differs from the oracle scan's (two different
+    eigen-solvers) must be a near-tie: its p lies inside the tie bracket [p_lo, p_hi] the
+    oracle's significance_treshold (css.c:675-752) gives on the DEVICE's own coordinates
+    and stream (permuted scores within 1e-11 |score| of the observed one counted both
+    ways; tests/test_css_perm_isolated.py).  Returns the number of mismatches."""
+    from gdscan import css
+    from test_css_perm_isolated import _oracle_p
+    bad = np.flatnonzero(p_dev != p_ref)
+    if bad.size == 0:
+        return 0
+    _, p2, X = css.scan_coords(av, bv, ap, bp, regend, treshold=treshold, runs=runs, seed=seed, serial=serial,
+                               mds=mds)
+    out = []
+    for w in bad:
+        assert p2[w] == p_dev[w], "scan and scan_coords disagree"
+        _, _, lo, hi, _ = _oracle_p(oracle, X[w], a, b, treshold, runs, seed, int(w))
+        if not lo <= p_dev[w] <= hi:
+            out.append((int(w), p_dev[w], p_ref[w], lo, hi))
+    assert not out, f"p mismatches outside the tie bracket: {out[:10]}"
+    return int(bad.size)

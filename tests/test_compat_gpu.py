@@ -6,7 +6,7 @@ import ctypes
 import numpy as np
 import pytest
 
-from conftest import PKG, close, oracle_css_scan, oracle_fet_scan
+from conftest import assert_p_mismatches_are_ties, PKG, close, oracle_css_scan, oracle_fet_scan
 
 pytestmark = pytest.mark.gpu
 
@@ -62,4 +62,6 @@ def test_css_compat_symbols(oracle, serial):
     assert np.array_equal(s != 0, comp)
     assert np.all(np.abs(s - s_ref) <= 1e-9 * np.abs(s_ref) + 1e-12)
     assert np.all(p[~comp] == -1.0)  # untouched at uncomputed windows
-    assert (p[comp] == p_ref[comp]).mean() >= 0.99
+    # every p that differs from the oracle scan's is a near-tie on the device's coordinates
+    assert_p_mismatches_are_ties(oracle, av, bv, ap, bp, regend, 10, 11, np.where(comp, p, 0.0),
+                                 np.where(comp, p_ref, 0.0), 10, 100, 4242, serial=serial)

@@ -10,7 +10,7 @@ import ctypes
 import numpy as np
 import pytest
 
-from conftest import close, oracle_css_scan
+from conftest import assert_p_mismatches_are_ties, close, oracle_css_scan
 
 pytestmark = pytest.mark.gpu
 
@@ -65,9 +65,10 @@ def test_permutation_p_matches_oracle(oracle, asize, bsize, treshold, runs, nsnp
     s_ref, p_ref = oracle_css_scan(oracle, av, bv, ap, bp, regend, treshold=treshold, runs=runs, seed=77)
     _cmp_scores(s, s_ref)
     comp = s_ref != 0
-    same = p[comp] == p_ref[comp]
-    assert same.mean() >= 0.995, same.mean()
     assert np.all(p[~comp] == 0)
+    # every p that differs from the oracle scan's is a near-tie on the device's coordinates
+    assert_p_mismatches_are_ties(oracle, av, bv, ap, bp, regend, asize, bsize, np.where(comp, p, 0.0),
+                                 np.where(comp, p_ref, 0.0), treshold, runs, 77)
 
 
 @pytest.mark.parametrize("asize,bsize,nsnp,nbad", [(8, 8, 20_000, 400), (40, 40, 3_000, 400), (20, 20, 10_000, 40),
@@ -150,7 +151,7 @@ def test_device_batch_api_matches_host(oracle):
         s_ref, p_ref = oracle_css_scan(oracle, av, bv, ap, bp, regend, runs=100, seed=2000 + i)
         n = regend // 500
         _cmp_scores(sc[w:w + n], s_ref)
-        assert (pv[w:w + n] == p_ref).mean() >= 0.99
+        assert_p_mismatches_are_ties(oracle, av, bv, ap, bp, regend, 10, 10, pv[w:w + n], p_ref, 10, 100, 2000 + i)
         w += n
 
 
@@ -194,7 +195,9 @@ def test_device_batch_mixed_cohorts(oracle, shapes):
         n = regend // 500
         _cmp_scores(sc[w:w + n], s_ref)
         comp = s_ref != 0
-        assert (pv[w:w + n][comp] == p_ref[comp]).mean() >= 0.99, i
+        a_, b_ = shapes[i][0], shapes[i][1]
+        assert_p_mismatches_are_ties(oracle, av, bv, ap, bp, regend, a_, b_, np.where(comp, pv[w:w + n], 0.0),
+                                     np.where(comp, p_ref, 0.0), 10, 60, 3000 + i)
         w += n
 
 
@@ -226,7 +229,7 @@ def test_dense_windows_multi_chunk(oracle):
     s, p = css.scan(av, bv, ap, bp, regend, treshold=5, runs=40, seed=3)
     s_ref, p_ref = oracle_css_scan(oracle, av, bv, ap, bp, regend, treshold=5, runs=40, seed=3)
     _cmp_scores(s, s_ref)
-    assert (p == p_ref).mean() >= 0.99
+    assert_p_mismatches_are_ties(oracle, av, bv, ap, bp, regend, 8, 8, p, p_ref, 5, 40, 3)
 
 
 def test_largest_tier_64_plus_64(oracle):
@@ -253,7 +256,9 @@ def test_serial_window_set_with_permutations(oracle):
     s, p = css.scan(av, bv, ap, bp, regend, treshold=10, runs=200, seed=9, serial=True)
     s_ref, p_ref = oracle_css_scan(oracle, av, bv, ap, bp, regend, treshold=10, runs=200, seed=9, serial=True)
     _cmp_scores(s, s_ref)
-    assert (p[s_ref != 0] == p_ref[s_ref != 0]).mean() >= 0.995
+    comp = s_ref != 0
+    assert_p_mismatches_are_ties(oracle, av, bv, ap, bp, regend, 9, 11, np.where(comp, p, 0.0),
+                                 np.where(comp, p_ref, 0.0), 10, 200, 9, serial=True)
 
 
 @pytest.mark.parametrize("asize,bsize,treshold,runs,nsnp,dup", [(10, 10, 100_000, 500, 15_000, False),

@@ -42,6 +42,48 @@ def oracle_scan_ex(orc, av, bv, ap, bp, regend, drosophila, mds, treshold=10, ru
     return s, p
 
 
+def assert_smacof2_mismatches_are_start_effects(orc, av, bv, ap, bp, regend, a, b, s_dev, s_ref, serial=False):
+    """mds 2 runs SMACOF from the classical coordinates (css.c:208-218).  The device's and
+    the oracle's classical coordinates come from different eigen-solvers (~1e-14 apart),
+    and a start that close can end one iteration apart at the 1e-6 exit test.  Every window
+    whose score misses the oracle's by more than 1e-9 must therefore equal, to 1e-9, the
+    oracle's SMACOF (css.c:767-938) re-run from the DEVICE's classical coordinates
+    (scan_coords, mds 0).  Returns the number of such windows."""
+    from gdscan import css
+    from conftest import window_slices
+    ok = (np.abs(s_dev - s_ref) <= 1e-9 * np.abs(s_ref) + 1e-12) | (np.isnan(s_dev) & np.isnan(s_ref))
+    bad = np.flatnonzero(~ok)
+    if bad.size == 0:
+        return 0
+    _, _, X0 = css.scan_coords(av, bv, ap, bp, regend, runs=0, serial=serial)
+    sl = window_slices(ap, bp, regend, a, b, serial=serial)
+    C = ctypes
+    orc.orc_css_compare_all.argtypes = [F64, F64, C.c_int, C.c_int, C.c_int, F64]
+    orc.orc_css_fill_averages.argtypes = [F64, C.c_int]
+    orc.orc_css_dist.argtypes = [F64, C.c_int, F64]
+    orc.orc_css_score.argtypes = [F64, C.c_int, np.ctypeslib.ndpointer(np.int32, flags="C"),
+                                  np.ctypeslib.ndpointer(np.int32, flags="C"), C.c_int, C.c_int]
+    orc.orc_css_score.restype = C.c_double
+    m = a + b
+    out = []
+    for w in bad:
+        la0, lb0, npos = sl[int(w)]
+        D = np.zeros(m * m)
+        orc.orc_css_compare_all(np.ascontiguousarray(av[la0:la0 + npos * a]),
+                                np.ascontiguousarray(bv[lb0:lb0 + npos * b]), a, b, npos, D)
+        assert orc.orc_css_fill_averages(D, m)
+        X = np.ascontiguousarray(X0[w].reshape(-1))
+        it = C.c_int()
+        orc.orc_css_smacof(D, m, X, 300, 0.000001, C.byref(it))
+        S = np.zeros(m * m)
+        orc.orc_css_dist(X, m, S)
+        sc = orc.orc_css_score(S, m, np.arange(a, dtype=np.int32), np.arange(a, m, dtype=np.int32), a, b)
+        if not abs(sc - s_dev[w]) <= 1e-9 * abs(sc) + 1e-12:
+            out.append((int(w), s_dev[w], s_ref[w], sc))
+    assert not out, f"mds 2 mismatches not explained by the start: {out[:10]}"
+    return int(bad.size)
+
+
 def freq_tracks(c, nsnp):
     """One allele-frequency value per population and SNP (the drosophila input, asize =
     bsize = 1), positions as the synthetic generator lays them out."""
@@ -133,8 +175,7 @@ def test_smacof_after_cmds_matches_oracle(opt):
     s, _ = css.scan(av, bv, ap, bp, regend, runs=0, mds=2)
     s_ref, _ = oracle_scan_ex(opt, av, bv, ap, bp, regend, 0, 2)
     assert np.array_equal(s == 0, s_ref == 0)
-    assert _close_frac(s, s_ref, 1e-9) >= 0.98
-    assert _close_frac(s, s_ref, 1e-4) == 1.0
+    assert_smacof2_mismatches_are_start_effects(opt, av, bv, ap, bp, regend, 8, 8, s, s_ref)
 
 
 @pytest.mark.gpu
@@ -145,7 +186,9 @@ def test_smacof_with_permutations(opt):
     s_ref, p_ref = oracle_scan_ex(opt, av, bv, ap, bp, regend, 0, 1, treshold=10, runs=200, seed=5)
     assert _close_frac(s, s_ref, 1e-9) == 1.0
     comp = s_ref != 0
-    assert (p[comp] == p_ref[comp]).mean() >= 0.99
+    from conftest import assert_p_mismatches_are_ties
+    assert_p_mismatches_are_ties(opt, av, bv, ap, bp, regend, 6, 6, np.where(comp, p, 0.0),
+                                 np.where(comp, p_ref, 0.0), 10, 200, 5, mds=1)
 
 
 @pytest.mark.gpu
@@ -158,8 +201,15 @@ def test_drosophila_metric_matches_oracle(opt, mds):
     assert np.array_equal(s == 0, s_ref == 0)
     assert (s_ref != 0).sum() > 5000
     assert _close_frac(s, s_ref, 1e-9) == 1.0
-    # two points: every permutation reproduces the observed distance up to rounding
-    assert (p[s_ref != 0] == p_ref[s_ref != 0]).mean() >= 0.99
+    # two points: a permutation keeps or swaps them, so every permuted score equals the
+    # observed one in exact arithmetic and only rounding decides hit or miss -- the tie
+    # bracket is the whole feasible range [1 / (runs + 1), 1]; a differing p must be a
+    # value the p = (hits + 1) / (permutations + 1) rule can produce
+    comp = s_ref != 0
+    diff = comp & (p != p_ref)
+    assert np.all((p[diff] >= 1.0 / 51) & (p[diff] <= 1.0))
+    for v in np.unique(p[diff]):
+        assert any(abs(v - (h + 1) / (n + 1)) < 1e-15 for n in range(1, 51) for h in range(0, min(n, 10) + 1))
 
 
 @pytest.mark.gpu
