@@ -23,6 +23,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <algorithm>
+#include <memory>
 #include <string>
 #include <thread>
 #include <unordered_map>
@@ -160,90 +161,120 @@ void parse_chunk(const char *p, const char *end, const Columns &col, Chunk *out)
 
 }  // namespace
 
-extern "C" gd_gtrack *gd_gtrack_read(const char *path) {
-  if (!path) {
-    gd_set_error("null path");
-    return nullptr;
-  }
-  const int fd = open(path, O_RDONLY);
-  if (fd < 0) {
-    gd_set_error((std::string("cannot open ") + path + ": " + strerror(errno)).c_str());
-    return nullptr;
-  }
-  struct stat st;
-  if (fstat(fd, &st) != 0) {
-    close(fd);
-    gd_set_error("fstat failed");
-    return nullptr;
-  }
-  const size_t size = (size_t)st.st_size;
+namespace {
+
+/* a GTrack file mapped read-only, its column header read (leading '#' lines: the "###"
+ * line names the columns) and its data split into up to 16 chunks at line boundaries */
+struct MappedTrack {
   const char *data = nullptr;
-  if (size > 0) {
-    void *m = mmap(nullptr, size, PROT_READ, MAP_PRIVATE, fd, 0);
-    if (m == MAP_FAILED) {
+  size_t size = 0;
+  Columns col;
+  std::vector<const char *> cut; /* chunk k is [cut[k], cut[k + 1]) */
+  std::string err;
+
+  ~MappedTrack() {
+    if (data) munmap((void *)data, size);
+  }
+
+  bool open_file(const char *path) {
+    if (!path) {
+      err = "null path";
+      return false;
+    }
+    const int fd = open(path, O_RDONLY);
+    if (fd < 0) {
+      err = std::string("cannot open ") + path + ": " + strerror(errno);
+      return false;
+    }
+    struct stat st;
+    if (fstat(fd, &st) != 0) {
       close(fd);
-      gd_set_error("mmap failed");
+      err = "fstat failed";
+      return false;
+    }
+    size = (size_t)st.st_size;
+    if (size > 0) {
+      void *m = mmap(nullptr, size, PROT_READ, MAP_PRIVATE, fd, 0);
+      if (m == MAP_FAILED) {
+        close(fd);
+        size = 0;
+        err = "mmap failed";
+        return false;
+      }
+      madvise(m, size, MADV_SEQUENTIAL);
+      data = (const char *)m;
+    }
+    close(fd);
+    const char *p = data, *end = data + size;
+    while (p < end && *p == '#') {
+      const char *nl = (const char *)memchr(p, '\n', (size_t)(end - p));
+      const char *le = nl ? nl : end;
+      const char *line_end = (le > p && le[-1] == '\r') ? le - 1 : le;
+      if (line_end - p > 3 && p[1] == '#' && p[2] == '#' && p[3] != '#') {
+        const char *fb[32], *fe[32];
+        const int n = split_tabs(p + 3, line_end, fb, fe, 32);
+        Columns c;
+        c.seqid = c.start = c.value = -1;
+        c.ncol = n;
+        for (int k = 0; k < n && k < 32; ++k) {
+          const std::string name(fb[k], fe[k]);
+          if (name == "seqid") c.seqid = k;
+          if (name == "start") c.start = k;
+          if (name == "value") c.value = k;
+        }
+        if (c.seqid < 0 || c.start < 0 || c.value < 0) err = std::string(path) + ": column header lacks seqid/start/value";
+        col = c;
+      }
+      p = nl ? nl + 1 : end;
+    }
+    if (!err.empty()) return false;
+    if (p < end) {
+      const size_t bytes = (size_t)(end - p);
+      /* one thread per 16 MiB, at most 16 (GD_GTRACK_CHUNK: bytes per thread, for tests) */
+      size_t per = (size_t)1 << 24;
+      if (const char *e = getenv("GD_GTRACK_CHUNK")) per = std::max<size_t>(1, strtoull(e, nullptr, 10));
+      const unsigned hw = std::thread::hardware_concurrency();
+      const int T = (int)std::min<size_t>(std::max(1u, std::min(hw, 16u)), std::max<size_t>(1, bytes / per));
+      cut.assign(T + 1, p);
+      cut[T] = end;
+      for (int k = 1; k < T; ++k) {
+        const char *q = p + bytes * k / T;
+        if (q < cut[k - 1]) q = cut[k - 1];
+        const char *nl = (const char *)memchr(q, '\n', (size_t)(end - q));
+        cut[k] = nl ? nl + 1 : end;
+      }
+    }
+    return true;
+  }
+
+  int chunks() const { return cut.empty() ? 0 : (int)cut.size() - 1; }
+
+  /* fn(k) on chunk k, chunks 1.. on their own threads */
+  template <class F>
+  void parallel(F fn) const {
+    std::vector<std::thread> th;
+    for (int k = 1; k < chunks(); ++k) th.emplace_back(fn, k);
+    if (chunks() > 0) fn(0);
+    for (auto &x : th) x.join();
+  }
+};
+
+}  // namespace
+
+extern "C" gd_gtrack *gd_gtrack_read(const char *path) {
+  MappedTrack mt;
+  if (!mt.open_file(path)) {
+    gd_set_error(mt.err.c_str());
+    return nullptr;
+  }
+  /* data: chunks parsed in parallel, runs merged in order */
+  std::vector<Chunk> chunks(mt.chunks());
+  mt.parallel([&](int k) { parse_chunk(mt.cut[k], mt.cut[k + 1], mt.col, &chunks[k]); });
+  for (auto &c : chunks)
+    if (!c.ok) {
+      gd_set_error((std::string(path) + ": " + c.err).c_str());
       return nullptr;
     }
-    madvise(m, size, MADV_SEQUENTIAL);
-    data = (const char *)m;
-  }
-  close(fd);
-
-  /* leading '#' lines: the "###" line names the columns */
-  Columns col;
-  const char *p = data, *end = data + size;
-  std::string err;
-  while (p < end && *p == '#') {
-    const char *nl = (const char *)memchr(p, '\n', (size_t)(end - p));
-    const char *le = nl ? nl : end;
-    const char *line_end = (le > p && le[-1] == '\r') ? le - 1 : le;
-    if (line_end - p > 3 && p[1] == '#' && p[2] == '#' && p[3] != '#') {
-      const char *fb[32], *fe[32];
-      const int n = split_tabs(p + 3, line_end, fb, fe, 32);
-      Columns c;
-      c.seqid = c.start = c.value = -1;
-      c.ncol = n;
-      for (int k = 0; k < n && k < 32; ++k) {
-        const std::string name(fb[k], fe[k]);
-        if (name == "seqid") c.seqid = k;
-        if (name == "start") c.start = k;
-        if (name == "value") c.value = k;
-      }
-      if (c.seqid < 0 || c.start < 0 || c.value < 0) err = "column header lacks seqid/start/value";
-      col = c;
-    }
-    p = nl ? nl + 1 : end;
-  }
-
-  /* data: chunks split at line boundaries, parsed in parallel, runs merged in order */
-  std::vector<Chunk> chunks;
-  if (err.empty() && p < end) {
-    const size_t bytes = (size_t)(end - p);
-    unsigned hw = std::thread::hardware_concurrency();
-    int T = (int)std::min<size_t>(std::max(1u, std::min(hw, 16u)), std::max<size_t>(1, bytes >> 24));
-    std::vector<const char *> cut(T + 1);
-    cut[0] = p;
-    cut[T] = end;
-    for (int k = 1; k < T; ++k) {
-      const char *q = p + bytes * k / T;
-      if (q < cut[k - 1]) q = cut[k - 1];
-      const char *nl = (const char *)memchr(q, '\n', (size_t)(end - q));
-      cut[k] = nl ? nl + 1 : end;
-    }
-    chunks.resize(T);
-    std::vector<std::thread> th;
-    for (int k = 1; k < T; ++k) th.emplace_back(parse_chunk, cut[k], cut[k + 1], std::cref(col), &chunks[k]);
-    parse_chunk(cut[0], cut[1], col, &chunks[0]);
-    for (auto &x : th) x.join();
-    for (auto &c : chunks)
-      if (!c.ok && err.empty()) err = c.err;
-  }
-  if (data) munmap((void *)data, size);
-  if (!err.empty()) {
-    gd_set_error((std::string(path) + ": " + err).c_str());
-    return nullptr;
-  }
   gd_gtrack *t = new gd_gtrack();
   std::unordered_map<std::string, int> index;
   for (auto &c : chunks)
@@ -285,6 +316,229 @@ extern "C" int gd_gtrack_copy(const gd_gtrack *t, int s, int32_t *starts, double
   const size_t n = t->starts[s].size();
   if (starts && n) memcpy(starts, t->starts[s].data(), n * sizeof(int32_t));
   if (vals && n) memcpy(vals, t->vals[s].data(), n * sizeof(double));
+  return GD_OK;
+}
+
+/* ------------------------------------------------------------------------------------
+ * Packing reader: the same files parsed straight into packed genotype tracks (2-bit
+ * codes, one position per row; include/gdscan.h "packed genotype tracks"), with no f64
+ * value or per-element position ever materialised.  The chunk parsers keep one byte per
+ * genotype and the positions run-length encoded (a row is a run of `size` equal
+ * positions); the merge joins the runs of each sequence in file order, takes the
+ * population size from the leading run (get_population_size, comparative.c:25-34) and
+ * checks every run holds whole rows; then each chunk packs its own bytes into the final
+ * words (words shared by two chunks are or-ed atomically).
+ */
+struct gd_ptrack {
+  std::vector<std::string> seqid;
+  std::vector<int32_t> size;
+  std::vector<std::vector<uint64_t>> codes; /* nrows * GD_PACK_WORDS(size) words */
+  std::vector<std::vector<int32_t>> rowpos; /* nrows */
+};
+
+namespace {
+
+struct PRun {
+  std::string seqid;
+  std::vector<uint8_t> codes; /* one per line */
+  std::vector<int32_t> rpos;  /* positions, run-length encoded */
+  std::vector<int64_t> rlen;
+  int seq = -1;
+  int64_t first = 0; /* index of codes[0] among its sequence's elements */
+};
+
+struct PChunk {
+  std::vector<PRun> runs;
+  bool ok = true;
+  std::string err;
+};
+
+/* VCFConvert.py:9-18 values -> GD_CODE_* */
+bool genotype_code(double x, uint8_t *c) {
+  if (x == 3.0)
+    *c = GD_CODE_MAJOR;
+  else if (x == -3.0)
+    *c = GD_CODE_MINOR;
+  else if (x == 0.0)
+    *c = GD_CODE_HET;
+  else if (x == -10000.0)
+    *c = GD_CODE_MISSING;
+  else
+    return false;
+  return true;
+}
+
+void parse_packed_chunk(const char *p, const char *end, const Columns &col, PChunk *out) {
+  PRun *cur = nullptr;
+  while (p < end) {
+    const char *nl = (const char *)memchr(p, '\n', (size_t)(end - p));
+    const char *le = nl ? nl : end;
+    const char *line_end = (le > p && le[-1] == '\r') ? le - 1 : le;
+    if (line_end > p && p[0] != '#') {
+      const char *fb[32], *fe[32];
+      const int n = split_tabs(p, line_end, fb, fe, 32);
+      int64_t pos;
+      double val;
+      uint8_t code;
+      if (n <= col.seqid || n <= col.start || n <= col.value || !parse_int(fb[col.start], fe[col.start], &pos) ||
+          pos < INT32_MIN || pos > INT32_MAX || !parse_value(fb[col.value], fe[col.value], &val)) {
+        out->ok = false;
+        out->err = "malformed data line: " + std::string(p, (size_t)std::min<ptrdiff_t>(line_end - p, 80));
+        return;
+      }
+      if (!genotype_code(val, &code)) {
+        out->ok = false;
+        out->err = "a value is not one of the genotype codes 3, 0, -3, -10000: " +
+                   std::string(p, (size_t)std::min<ptrdiff_t>(line_end - p, 80));
+        return;
+      }
+      const size_t nlen = (size_t)(fe[col.seqid] - fb[col.seqid]);
+      if (!cur || nlen != cur->seqid.size() || memcmp(fb[col.seqid], cur->seqid.data(), nlen) != 0) {
+        out->runs.emplace_back();
+        cur = &out->runs.back();
+        cur->seqid.assign(fb[col.seqid], nlen);
+      }
+      cur->codes.push_back(code);
+      if (!cur->rpos.empty() && cur->rpos.back() == (int32_t)pos) {
+        ++cur->rlen.back();
+      } else {
+        cur->rpos.push_back((int32_t)pos);
+        cur->rlen.push_back(1);
+      }
+    }
+    p = nl ? nl + 1 : end;
+  }
+}
+
+/* or the run's codes into its sequence's words: element e of the sequence is individual
+ * e mod size of row e / size */
+void pack_run(const PRun &r, int64_t size, uint64_t *words) {
+  const int64_t W = GD_PACK_WORDS(size);
+  int64_t row = r.first / size, k = r.first % size;
+  int64_t widx = row * W + (k >> 5);
+  uint64_t acc = 0;
+  for (uint8_t c : r.codes) {
+    acc |= (uint64_t)c << (2 * (k & 31));
+    if (++k == size) {
+      __atomic_fetch_or(&words[widx], acc, __ATOMIC_RELAXED);
+      acc = 0;
+      k = 0;
+      ++row;
+      widx = row * W;
+    } else if ((k & 31) == 0) {
+      __atomic_fetch_or(&words[widx], acc, __ATOMIC_RELAXED);
+      acc = 0;
+      ++widx;
+    }
+  }
+  if (acc) __atomic_fetch_or(&words[widx], acc, __ATOMIC_RELAXED);
+}
+
+}  // namespace
+
+extern "C" gd_ptrack *gd_ptrack_read(const char *path) {
+  MappedTrack mt;
+  if (!mt.open_file(path)) {
+    gd_set_error(mt.err.c_str());
+    return nullptr;
+  }
+  std::vector<PChunk> chunks(mt.chunks());
+  mt.parallel([&](int k) { parse_packed_chunk(mt.cut[k], mt.cut[k + 1], mt.col, &chunks[k]); });
+  for (auto &c : chunks)
+    if (!c.ok) {
+      gd_set_error((std::string(path) + ": " + c.err).c_str());
+      return nullptr;
+    }
+  /* merge: the runs of each sequence in file order, their position runs joined */
+  std::unique_ptr<gd_ptrack> t(new gd_ptrack());
+  std::unordered_map<std::string, int> index;
+  std::vector<std::vector<int32_t>> rpos;
+  std::vector<std::vector<int64_t>> rlen;
+  std::vector<int64_t> nel;
+  for (auto &c : chunks)
+    for (auto &r : c.runs) {
+      auto it = index.find(r.seqid);
+      if (it == index.end()) {
+        it = index.emplace(r.seqid, (int)t->seqid.size()).first;
+        t->seqid.push_back(r.seqid);
+        rpos.emplace_back();
+        rlen.emplace_back();
+        nel.push_back(0);
+      }
+      const int s = it->second;
+      r.seq = s;
+      r.first = nel[s];
+      nel[s] += (int64_t)r.codes.size();
+      for (size_t j = 0; j < r.rpos.size(); ++j) {
+        if (!rpos[s].empty() && rpos[s].back() == r.rpos[j]) {
+          rlen[s].back() += r.rlen[j];
+        } else {
+          rpos[s].push_back(r.rpos[j]);
+          rlen[s].push_back(r.rlen[j]);
+        }
+      }
+      std::vector<int32_t>().swap(r.rpos);
+      std::vector<int64_t>().swap(r.rlen);
+    }
+  const int ns = (int)t->seqid.size();
+  t->size.resize(ns);
+  t->codes.resize(ns);
+  t->rowpos.resize(ns);
+  for (int s = 0; s < ns; ++s) {
+    const int64_t size = rlen[s][0];
+    if (size > INT32_MAX) {
+      gd_set_error((std::string(path) + ": population size above 2^31 in sequence " + t->seqid[s]).c_str());
+      return nullptr;
+    }
+    std::vector<int32_t> &rp = t->rowpos[s];
+    rp.reserve((size_t)(nel[s] / size));
+    for (size_t j = 0; j < rpos[s].size(); ++j) {
+      if (rlen[s][j] % size != 0) {
+        gd_set_error((std::string(path) + ": sequence " + t->seqid[s] + " does not consist of whole rows of " +
+                      std::to_string(size) + " individuals at one position (position " +
+                      std::to_string(rpos[s][j]) + " holds " + std::to_string(rlen[s][j]) +
+                      " elements); such a track keeps the reference layout (gd_gtrack_read)")
+                         .c_str());
+        return nullptr;
+      }
+      rp.insert(rp.end(), (size_t)(rlen[s][j] / size), rpos[s][j]);
+    }
+    t->size[s] = (int32_t)size;
+    t->codes[s].assign(rp.size() * (size_t)GD_PACK_WORDS(size), 0);
+    std::vector<int32_t>().swap(rpos[s]);
+    std::vector<int64_t>().swap(rlen[s]);
+  }
+  mt.parallel([&](int k) {
+    for (const PRun &r : chunks[k].runs) pack_run(r, t->size[r.seq], t->codes[r.seq].data());
+  });
+  return t.release();
+}
+
+extern "C" void gd_ptrack_free(gd_ptrack *t) { delete t; }
+
+extern "C" int gd_ptrack_nseq(const gd_ptrack *t) { return t ? (int)t->seqid.size() : 0; }
+
+extern "C" const char *gd_ptrack_seqid(const gd_ptrack *t, int s) {
+  return (t && s >= 0 && s < (int)t->seqid.size()) ? t->seqid[s].c_str() : nullptr;
+}
+
+extern "C" int gd_ptrack_shape(const gd_ptrack *t, int s, int32_t *size, int64_t *nrows) {
+  if (!t || s < 0 || s >= (int)t->seqid.size() || !size || !nrows) {
+    gd_set_error("bad sequence index");
+    return GD_ERR_ARG;
+  }
+  *size = t->size[s];
+  *nrows = (int64_t)t->rowpos[s].size();
+  return GD_OK;
+}
+
+extern "C" int gd_ptrack_copy(const gd_ptrack *t, int s, uint64_t *codes, int32_t *rowpos) {
+  if (!t || s < 0 || s >= (int)t->seqid.size()) {
+    gd_set_error("bad sequence index");
+    return GD_ERR_ARG;
+  }
+  if (codes && !t->codes[s].empty()) memcpy(codes, t->codes[s].data(), t->codes[s].size() * sizeof(uint64_t));
+  if (rowpos && !t->rowpos[s].empty()) memcpy(rowpos, t->rowpos[s].data(), t->rowpos[s].size() * sizeof(int32_t));
   return GD_OK;
 }
 

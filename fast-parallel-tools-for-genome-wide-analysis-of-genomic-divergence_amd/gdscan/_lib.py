@@ -39,6 +39,7 @@ EXPORTS = (
     "gd_set_seed", "gd_get_seed", "gd_last_error", "gd_device_count",
     "gd_last_stage_ms", "gd_synth_device",
     "gd_gtrack_read", "gd_gtrack_free", "gd_gtrack_nseq", "gd_gtrack_seqid", "gd_gtrack_len", "gd_gtrack_copy",
+    "gd_ptrack_read", "gd_ptrack_free", "gd_ptrack_nseq", "gd_ptrack_seqid", "gd_ptrack_shape", "gd_ptrack_copy",
     "gd_write_tabular", "gd_format_py2_float",
     "gd_tabular_read", "gd_tabular_free", "gd_tabular_rows", "gd_tabular_nseq", "gd_tabular_seqid",
     "gd_tabular_copy",
@@ -135,6 +136,15 @@ def _load() -> C.CDLL:
     lib.gd_gtrack_len.argtypes = [vp, i32]
     lib.gd_gtrack_len.restype = C.c_int64
     lib.gd_gtrack_copy.argtypes = [vp, i32, vp, vp]
+    lib.gd_ptrack_read.argtypes = [C.c_char_p]
+    lib.gd_ptrack_read.restype = vp
+    lib.gd_ptrack_free.argtypes = [vp]
+    lib.gd_ptrack_free.restype = None
+    lib.gd_ptrack_nseq.argtypes = [vp]
+    lib.gd_ptrack_seqid.argtypes = [vp, i32]
+    lib.gd_ptrack_seqid.restype = C.c_char_p
+    lib.gd_ptrack_shape.argtypes = [vp, i32, C.POINTER(C.c_int32), C.POINTER(C.c_int64)]
+    lib.gd_ptrack_copy.argtypes = [vp, i32, vp, vp]
     lib.gd_write_tabular.argtypes = [C.c_char_p, i32, C.c_char_p, C.c_char_p, i32, C.c_int64, vp, vp]
     lib.gd_format_py2_float.argtypes = [C.c_double, C.c_char_p, i32]
     i64, pi64 = C.c_int64, C.POINTER(C.c_int64)
@@ -168,7 +178,8 @@ def _load() -> C.CDLL:
     for fn in ("gd_pack_shape", "gd_pack_chrom", "gd_pack_chrom_device", "gd_fet_scan_packed_device",
                "gd_css_scan_packed_device", "gd_fet_scan_packed_host", "gd_css_scan_packed_host"):
         getattr(lib, fn).restype = C.c_int
-    for fn in ("gd_gtrack_nseq", "gd_gtrack_copy", "gd_write_tabular", "gd_format_py2_float"):
+    for fn in ("gd_gtrack_nseq", "gd_gtrack_copy", "gd_write_tabular", "gd_format_py2_float", "gd_ptrack_nseq",
+               "gd_ptrack_shape", "gd_ptrack_copy"):
         getattr(lib, fn).restype = C.c_int
     for fn in ("gd_fet_threadcompute", "gd_fet_compute", "gd_fet_scan_host", "gd_css_threadcompute",
                "gd_css_compute", "gd_css_scan_host", "gd_css_scan_host_ex", "gd_fet_scan_device",

@@ -3,6 +3,8 @@
 read_gtrack       GTrack "valued points" file -> per-seqid (starts int32, vals float64),
                   the arrays HyperBrowser's startsAsNumpyArray / valsAsNumpyArray give the
                   statistics (native parser in lib/libgdscan.so, gd_gtrack.cpp).
+read_gtrack_packed  the same file parsed straight into packed genotype tracks (2-bit
+                  codes, one position per row; gd_ptrack_read), no f64 intermediate.
 write_tabular     the tools' result lines (FisherExactTestSNPTool.py:162-189,
                   ClusterSeparationScore.py:180-205), floats as Python 2 str() (Q11).
 vcf_to_gtrack     restatement of tools/VCFConvert.py:2-86 (genotype -> 3 / 0 / -3 / -10000).
@@ -37,6 +39,31 @@ def read_gtrack(path) -> "OrderedDict[str, tuple[np.ndarray, np.ndarray]]":
         return out
     finally:
         lib.gd_gtrack_free(h)
+
+
+def read_gtrack_packed(path) -> "OrderedDict[str, tuple[np.ndarray, np.ndarray, int]]":
+    """seqid -> (rowpos int32 [nrows], codes uint64 [nrows * words(size)], size): the
+    packed form of read_gtrack's arrays (gdscan.packed layout).  ValueError for a track
+    with no packed form (a value other than 3, 0, -3, -10000, or positions not in whole
+    rows of get_population_size() individuals); GdError for an unreadable file."""
+    h = lib.gd_ptrack_read(str(path).encode())
+    if not h:
+        msg = lib.gd_last_error().decode(errors="replace")
+        if "genotype codes" in msg or "whole rows" in msg:
+            raise ValueError(msg)
+        raise GdError(-1, msg)
+    try:
+        out = OrderedDict()
+        size, nrows = C.c_int32(), C.c_int64()
+        for s in range(lib.gd_ptrack_nseq(h)):
+            check(lib.gd_ptrack_shape(h, s, C.byref(size), C.byref(nrows)))
+            rowpos = np.empty(nrows.value, dtype=np.int32)
+            codes = np.empty(nrows.value * ((size.value + 31) // 32), dtype=np.uint64)
+            check(lib.gd_ptrack_copy(h, s, codes.ctypes.data, rowpos.ctypes.data))
+            out[lib.gd_ptrack_seqid(h, s).decode()] = (rowpos, codes, size.value)
+        return out
+    finally:
+        lib.gd_ptrack_free(h)
 
 
 def py2_str(x: float) -> str:

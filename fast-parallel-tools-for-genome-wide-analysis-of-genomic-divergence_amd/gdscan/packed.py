@@ -90,6 +90,28 @@ def pack(avals, bvals, apos, bpos, regend):
     return PackedChrom(ac, bc, rp, asize, bsize, int(regend))
 
 
+def read_pair(track_a, track_b, chrom_lengths=None):
+    """Two population GTrack files read straight into packed chromosomes
+    (gtrack.read_gtrack_packed): (names, [PackedChrom]) for the sequences of A, in A's
+    order, that B also holds -- the chromosomes gdscan.tools scans, region
+    [0, chrom_lengths[seqid]) or [0, last position + 1).  ValueError when either file, or
+    a shared sequence of the pair (different rows in A and B), has no packed form."""
+    from .gtrack import read_gtrack_packed
+    ta, tb = read_gtrack_packed(track_a), read_gtrack_packed(track_b)
+    names, chroms = [], []
+    for s, (pa, ca, na) in ta.items():
+        if s not in tb or pa.shape[0] == 0:
+            continue
+        pb, cb, nb = tb[s]
+        if pa.shape[0] != pb.shape[0] or not np.array_equal(pa, pb):
+            raise ValueError(f"sequence {s}: the rows of A and B are not at the same positions "
+                             f"({pa.shape[0]} and {pb.shape[0]} rows); the pair keeps the reference layout")
+        regend = int(chrom_lengths[s]) if chrom_lengths and s in chrom_lengths else int(pa[-1]) + 1
+        names.append(s)
+        chroms.append(PackedChrom(ca, cb, pa, int(na), int(nb), regend))
+    return names, chroms
+
+
 def _batch(chroms, wstep, seed):
     """Concatenated codes / positions and the gd_pchrom descriptors; window outputs of
     chromosome c start at the running sum of regend // wstep."""

@@ -37,12 +37,29 @@ def _batch(track_a, track_b, wstep, chrom_lengths):
     return names, chroms, cat(av, np.float64), cat(bv, np.float64), cat(ap, np.int32), cat(bp, np.int32), w
 
 
-def _write(out_path, header, names, chroms, wstep, s0, s1):
+def _write(out_path, header, names, regends, wstep, s0, s1):
     write_tabular(out_path, names[0] if names else "", wstep, np.zeros(0), np.zeros(0), header=header, append=False)
-    for c, s in enumerate(names):
-        lo = chroms[c].w_out
-        n = chroms[c].regend // wstep
+    lo = 0
+    for s, regend in zip(names, regends):
+        n = regend // wstep
         write_tabular(out_path, s, wstep, s0[lo:lo + n], s1[lo:lo + n])
+        lo += n
+
+
+def _packed_pair(track_a, track_b, chrom_lengths, packed):
+    """The pair read straight into packed chromosomes (packed.read_pair) when `packed` is
+    True, or "auto" and both files have a packed form; None selects the reference layout."""
+    if packed is False:
+        return None
+    if packed not in (True, "auto"):
+        raise ValueError(f"packed must be True, False or 'auto', not {packed!r}")
+    from .packed import read_pair
+    try:
+        return read_pair(track_a, track_b, chrom_lengths)
+    except ValueError:
+        if packed is True:
+            raise
+        return None
 
 
 def _ptr(a, ct):
@@ -51,8 +68,20 @@ def _ptr(a, ct):
 
 
 def fisher_exact_test_snp(track_a, track_b, out_path, wsize=2500, wstep=500, percentile=0.95, chrom_lengths=None,
-                          exact=None):
+                          exact=None, packed="auto"):
+    """packed: "auto" reads genotype tracks straight into 2-bit codes (gdscan.packed; same
+    windows, scores and bootstrap streams) and falls back to the reference layout for
+    tracks with no packed form; True requires the packed form, False never uses it."""
     import ctypes as C
+    pair = _packed_pair(track_a, track_b, chrom_lengths, packed)
+    if pair is not None:
+        from . import packed as pk
+        names, pcs = pair
+        res = pk.fet_scan(pcs, wsize, wstep, percentile, exact=exact) if names else []
+        scores = np.concatenate([r[0] for r in res]) if res else np.zeros(0)
+        stddev = np.concatenate([r[1] for r in res]) if res else np.zeros(0)
+        _write(out_path, "#seqid\tstart\tscore\tstddev", names, [p.regend for p in pcs], wstep, scores, stddev)
+        return names, scores, stddev
     names, chroms, av, bv, ap, bp, w = _batch(track_a, track_b, wstep, chrom_lengths)
     scores, stddev = np.zeros(w), np.zeros(w)
     if names:
@@ -61,7 +90,8 @@ def fisher_exact_test_snp(track_a, track_b, out_path, wsize=2500, wstep=500, per
                                             _ptr(ap, C.c_int), _ptr(bp, C.c_int), int(wsize), int(wstep),
                                             float(percentile), mode, GD_WINDOWS_THREADED,
                                             _ptr(scores, C.c_double), _ptr(stddev, C.c_double)))
-    _write(out_path, "#seqid\tstart\tscore\tstddev", names, chroms, wstep, scores, stddev)
+    _write(out_path, "#seqid\tstart\tscore\tstddev", names, [chroms[c].regend for c in range(len(names))], wstep,
+           scores, stddev)
     return names, scores, stddev
 
 
@@ -71,14 +101,27 @@ MDS = {"classical": 0, "Classical MDS": 0, "smacof": 1, "SMACOF": 1, "smacof+cmd
 
 
 def cluster_separation_score(track_a, track_b, out_path, wsize=2500, wstep=500, mc_treshold=10, mc_runs=0,
-                             compare="count", mds="classical", chrom_lengths=None):
+                             compare="count", mds="classical", chrom_lengths=None, packed="auto"):
     """compare: "count" (SNP differences) or "freq" (drosophila allele-frequency metric,
     one frequency track per population); mds: "classical", "smacof" or "smacof+cmds"
-    (any other label selects SMACOF + classical, as the tool's else branch does)."""
+    (any other label selects SMACOF + classical, as the tool's else branch does);
+    packed: as fisher_exact_test_snp (the count metric only: "freq" tracks hold
+    frequencies, never genotype codes)."""
     import ctypes as C
     if compare not in COMPARE:
         raise ValueError(f"unknown distance metric {compare!r}")
     dro, md = COMPARE[compare], MDS.get(mds, 2)
+    pair = _packed_pair(track_a, track_b, chrom_lengths, packed) if dro == 0 else None
+    if dro and packed is True:
+        raise ValueError("the freq metric has no packed form")
+    if pair is not None:
+        from . import packed as pk
+        names, pcs = pair
+        res = pk.css_scan(pcs, wsize, wstep, mc_treshold, mc_runs, md) if names else []
+        scores = np.concatenate([r[0] for r in res]) if res else np.zeros(0)
+        p = np.concatenate([r[1] for r in res]) if res else np.zeros(0)
+        _write(out_path, "#seqid\tstart\tscore\tp", names, [c.regend for c in pcs], wstep, scores, p)
+        return names, scores, p
     names, chroms, av, bv, ap, bp, w = _batch(track_a, track_b, wstep, chrom_lengths)
     scores, p = np.zeros(w), np.zeros(w)
     if names:
@@ -86,5 +129,6 @@ def cluster_separation_score(track_a, track_b, out_path, wsize=2500, wstep=500, 
                                             _ptr(ap, C.c_int), _ptr(bp, C.c_int), int(wsize), int(wstep),
                                             int(mc_treshold), int(mc_runs), dro, md, GD_WINDOWS_THREADED,
                                             _ptr(scores, C.c_double), _ptr(p, C.c_double)))
-    _write(out_path, "#seqid\tstart\tscore\tp", names, chroms, wstep, scores, p)
+    _write(out_path, "#seqid\tstart\tscore\tp", names, [chroms[c].regend for c in range(len(names))], wstep,
+           scores, p)
     return names, scores, p

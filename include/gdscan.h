@@ -264,6 +264,21 @@ int gd_gtrack_nseq(const gd_gtrack *t);                   /* sequences, in first
 const char *gd_gtrack_seqid(const gd_gtrack *t, int s);
 int64_t gd_gtrack_len(const gd_gtrack *t, int s);         /* elements of sequence s */
 int gd_gtrack_copy(const gd_gtrack *t, int s, int32_t *starts, double *vals);
+/* the same files parsed straight into packed genotype tracks (2-bit codes, one position
+ * per row; no f64 intermediate): per sequence, size = get_population_size() (the leading
+ * run of equal positions, comparative.c:25-34) and nrows rows of `size` individuals at one
+ * position.  NULL (gd_last_error) for a track with no packed form -- a value other than
+ * 3, 0, -3, -10000, or a sequence whose positions do not come in whole rows -- which keeps
+ * the reference layout (gd_gtrack_read).  A pair of tracks scans packed (gd_pchrom) when
+ * each shared sequence has the same rowpos in both. */
+typedef struct gd_ptrack gd_ptrack;
+gd_ptrack *gd_ptrack_read(const char *path);
+void gd_ptrack_free(gd_ptrack *t);
+int gd_ptrack_nseq(const gd_ptrack *t); /* sequences, in first-seen order */
+const char *gd_ptrack_seqid(const gd_ptrack *t, int s);
+int gd_ptrack_shape(const gd_ptrack *t, int s, int32_t *size, int64_t *nrows);
+/* codes: nrows * GD_PACK_WORDS(size) words; rowpos: nrows */
+int gd_ptrack_copy(const gd_ptrack *t, int s, uint64_t *codes, int32_t *rowpos);
 /* appends (or creates) `path`: optional header line, then one line per window with
  * scores[i] != 0: "seqid\t<i*wstep>\t<score>\t<other>", floats as Python 2 str() */
 int gd_write_tabular(const char *path, int append, const char *header, const char *seqid, int wstep, int64_t n,

@@ -86,6 +86,77 @@ def test_read_gtrack_errors(tmp_path):
         read_gtrack(f)
 
 
+def _track_file(path, seqs, size):
+    """seqs: [(name, positions per element, values per element)] -> a GTrack file"""
+    from gdscan.gtrack import gtrack_header
+    lines = [gtrack_header("g")]
+    for name, pos, val in seqs:
+        lines += ["%s\t%d\t%d\tind%d\n" % (name, pos[k], val[k], k % size) for k in range(len(pos))]
+    path.write_text("".join(lines))
+    return path
+
+
+@pytest.mark.parametrize("chunk", [None, "4096", "777"])
+@pytest.mark.parametrize("size", [5, 32, 33, 70])
+def test_read_gtrack_packed_equals_pack_of_read_gtrack(tmp_path, monkeypatch, chunk, size):
+    """gd_ptrack_read against gd_pack_chrom of gd_gtrack_read's arrays, with the file cut
+    into many parser chunks (GD_GTRACK_CHUNK bytes per thread: rows and words split
+    across chunks), sequences interleaved and revisited."""
+    from gdscan import packed, synth
+    from gdscan.gtrack import read_gtrack, read_gtrack_packed
+    av, bv, ap, bp, _ = synth.chromosome(11, 600, size, size)
+    n = len(ap)
+    cut = (n // size // 3) * size
+    seqs = [("chrX", ap[:cut], av[:cut]), ("chr7", bp[:cut], bv[:cut]), ("chrX", ap[cut:], av[cut:]),
+            ("chr7", bp[cut:], bv[cut:])]
+    f = _track_file(tmp_path / "t.gtrack", seqs, size)
+    if chunk:
+        monkeypatch.setenv("GD_GTRACK_CHUNK", chunk)
+    ref, got = read_gtrack(f), read_gtrack_packed(f)
+    assert list(got) == list(ref) == ["chrX", "chr7"]
+    for s in ref:
+        pos, val = ref[s]
+        pc = packed.pack(val, val, pos, pos, int(pos[-1]) + 1)
+        rowpos, codes, sz = got[s]
+        assert sz == size and np.array_equal(rowpos, pc.rowpos) and np.array_equal(codes, pc.acodes)
+
+
+def test_read_gtrack_packed_duplicate_positions_and_errors(tmp_path):
+    """Two rows at one position stay two rows when the leading run is one row; the
+    population size is the leading run of equal positions (get_population_size), so a
+    track whose later run is not a multiple of it has no packed form (ValueError), and
+    so has a value outside 3, 0, -3, -10000."""
+    from gdscan import GdError, packed
+    from gdscan.gtrack import read_gtrack, read_gtrack_packed
+    vals = [3, 0, -3, -10000, 3, 3, 0, 0, -3]
+    f = _track_file(tmp_path / "dup.gtrack", [("c", [5, 5, 5, 9, 9, 9, 9, 9, 9], vals)], 3)
+    rowpos, codes, size = read_gtrack_packed(f)["c"]
+    assert size == 3 and rowpos.tolist() == [5, 9, 9]
+    pos, val = read_gtrack(f)["c"]
+    assert np.array_equal(codes, packed.pack(val, val, pos, pos, 10).acodes)
+    bad = _track_file(tmp_path / "ragged.gtrack", [("c", [5, 5, 9, 9, 9], [3, 3, 3, 3, 3])], 2)
+    with pytest.raises(ValueError, match="whole rows"):
+        read_gtrack_packed(bad)
+    freq = _track_file(tmp_path / "freq.gtrack", [("c", [5, 5], [3, 2])], 2)
+    with pytest.raises(ValueError, match="genotype codes"):
+        read_gtrack_packed(freq)
+    with pytest.raises(GdError):
+        read_gtrack_packed(tmp_path / "nope.gtrack")
+    assert len(read_gtrack_packed(_track_file(tmp_path / "empty.gtrack", [], 1))) == 0
+
+
+def test_read_pair_checks_rows(tmp_path):
+    from gdscan import packed
+    a = _track_file(tmp_path / "a.gtrack", [("c1", [1, 1, 4, 4], [3, 0, 0, 3]), ("c2", [2, 2], [3, 3])], 2)
+    b = _track_file(tmp_path / "b.gtrack", [("c2", [2, 2, 2], [0, 0, 0]), ("c1", [1, 1, 1, 4, 4, 4], [3] * 6)], 3)
+    names, pcs = packed.read_pair(a, b, {"c1": 1000})
+    assert names == ["c1", "c2"] and [p.regend for p in pcs] == [1000, 3]
+    assert (pcs[0].asize, pcs[0].bsize, pcs[0].nrows) == (2, 3, 2)
+    c = _track_file(tmp_path / "c.gtrack", [("c1", [1, 1, 1, 5, 5, 5], [3] * 6)], 3)
+    with pytest.raises(ValueError, match="same positions"):
+        packed.read_pair(a, c)
+
+
 def test_write_tabular_matches_tool_loop(tmp_path):
     """FisherExactTestSNPTool.py:162-189: header, then windows with score != 0 at i*wStep."""
     from gdscan.gtrack import write_tabular
