@@ -382,9 +382,11 @@ typedef float pm_f32x16 __attribute__((ext_vector_type(16)));
  * the accumulator tiles (lane l holds column l & 31, rows (reg & 3) + 8 (reg >> 2) +
  * 4 (l >> 5) of each 32 x 32 tile).  The consecutive within-group pairs (Q8) are gathered
  * from the same matrix.  Error bound, u = 2^-24: an entry is within 2^-10 of its scaled
- * value plus 2^-25 absolute (fp16 subnormals; a float rounding first); the products with
+ * value plus 2^-14 absolute (entries below fp16's smallest normal 2^-14 are stored as 0,
+ * so the bound holds whether or not the matrix cores keep fp16 denormals; a float
+ * rounding first); the products with
  * 0/1 are exact; each Y entry takes <= 16 KT fp32 roundings and each dot <= 32 MT + 1
- * more, so |bet - est| <= (2^-10 + u (16 KT + 32 MT + 4)) bet + a b 2^-25 / sc; the pair
+ * more, so |bet - est| <= (2^-10 + u (16 KT + 32 MT + 4)) bet + a b 2^-14 / sc; the pair
  * sums likewise with their term counts.  est and err as score_f32: |score_exact - est|
  * <= err, and the few lanes inside the bound recompute in FP64. */
 template <int MP>
@@ -514,7 +516,7 @@ __device__ __forceinline__ void score_mfma(const char *s16, const uint2 *lut, co
   const double ab = (double)(a * b), apb = (double)(a + b);
   const double dq = (double)q * inv_sc, dwa = (double)wa * inv_sc, dwb = (double)wb * inv_sc;
   est = dq / ab - apb * (dwa * inva + dwb * invb);
-  constexpr double U = 0x1p-24, REP = 0x1p-10, SUB = 0x1p-25;
+  constexpr double U = 0x1p-24, REP = 0x1p-10, SUB = 0x1p-14;
   const double ebet = (REP + U * (16 * KT + 32 * MT + 4)) * dq * 1.001 + SUB * ab * inv_sc;
   const double ewa = (REP + U * (a + 4)) * dwa * 1.001 + SUB * a * inv_sc;
   const double ewb = (REP + U * (b + 4)) * dwb * 1.001 + SUB * b * inv_sc;
@@ -898,6 +900,7 @@ __global__ void __launch_bounds__(PermShape<MP>::NT) PERM_WPE
         if (row < m && k < m && row != k) {
           const float dx = (float)(s_X[2 * row] - s_X[2 * k]), dy = (float)(s_X[2 * row + 1] - s_X[2 * k + 1]);
           v = __fsqrt_rn(dx * dx + dy * dy) * scf;
+          if (v < 0x1p-14f) v = 0.f; /* no fp16 denormals (score_mfma's SUB) */
         }
         *reinterpret_cast<_Float16 *>(s_U + row * SH::RS + 2 * k) = (_Float16)v;
       }
@@ -1255,16 +1258,36 @@ __device__ __forceinline__ double pb_wave_sum(double v) {
   return v;
 }
 
-/* css() (css.c:608-647) of one track array by one wave: S(x, y) at y ld + x */
+/* css() (css.c:608-647) of one track array by one wave: S(x, y) at y ld + x.
+ * The consecutive within-group pairs (Q8) in track order; the between-group sum over the
+ * pairs (A_i, B_j) of the two groups' members in ascending order, pair p = i b + j dealt
+ * to lane p mod 64 and summed in p order per lane (score_exact_wave's order): a function
+ * of the groups' SETS, so a permutation that keeps them scores the observed value bit for
+ * bit and its tie is decided as at the register tiers.  fl: m membership bytes, la / lb:
+ * the members ascending (the wave's LDS scratch). */
 template <class TRK>
 __device__ __forceinline__ double pb_score(TRK track, const double *S, int ld, int a, int b, double inva, double invb,
-                                           int lane) {
+                                           int lane, uint8_t *fl, uint16_t *la, uint16_t *lb) {
   const int ab = a * b, m = a + b;
+  for (int k = lane; k < m; k += 64) fl[track(k)] = (uint8_t)(k < a);
+  __builtin_amdgcn_wave_barrier();
+  const uint64_t below = (1ull << lane) - 1ull;
+  int na = 0, nb = 0;
+  for (int i0 = 0; i0 < m; i0 += 64) {
+    const int i = i0 + lane;
+    const bool v = i < m, in = v && fl[i] != 0;
+    const uint64_t A = __ballot(in), B = __ballot(v && !in);
+    if (in) la[na + __popcll(A & below)] = (uint16_t)i;
+    if (v && !in) lb[nb + __popcll(B & below)] = (uint16_t)i;
+    na += __popcll(A);
+    nb += __popcll(B);
+  }
+  __builtin_amdgcn_wave_barrier();
   double bet = 0.0, wa = 0.0, wb = 0.0;
   int ii = lane / b, jj = lane - (lane / b) * b;
 #pragma unroll 4
   for (int p = lane; p < ab; p += 64) {
-    bet += S[(int64_t)track(a + jj) * ld + track(ii)];
+    bet += S[(int64_t)lb[jj] * ld + la[ii]];
     jj += 64;
     while (jj >= b) {
       jj -= b;
@@ -1279,6 +1302,7 @@ __device__ __forceinline__ double pb_score(TRK track, const double *S, int ld, i
   bet = pb_wave_sum(bet);
   wa = pb_wave_sum(wa);
   wb = pb_wave_sum(wb);
+  __builtin_amdgcn_wave_barrier(); /* the scratch is rewritten by the wave's next score */
   return bet / (double)ab - (double)m * (wa * inva + wb * invb);
 }
 }  // namespace
@@ -1299,6 +1323,11 @@ __global__ void __launch_bounds__(256)
   __shared__ int64_t s_w;
   __shared__ int s_ctl[3]; /* hits, permutations run, done */
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  /* pb_score's scratch over s_X (dead once S is in the slab): per wave MP u16 for the
+   * members ascending (group A's, then group B's at offset a) and MP membership bytes */
+  static_assert(NT / 64 * 3 * MP <= (int)sizeof(s_X), "pb_score scratch");
+  uint16_t *s_ls = reinterpret_cast<uint16_t *>(s_X) + wave * MP;
+  uint8_t *s_fl = reinterpret_cast<uint8_t *>(s_X) + (NT / 64) * 2 * MP + wave * MP;
   double *S = slab + (int64_t)blockIdx.x * slab_per_wg;
   for (int n = tid; n <= MP; n += NT) s_mag[n] = gd_randint_make(n < 1 ? 1u : (uint32_t)n).magic;
 
@@ -1327,7 +1356,7 @@ __global__ void __launch_bounds__(256)
     const double inva = a > 1 ? 1.0 / (double)(a * a * (a - 1)) : 0.0;
     const double invb = b > 1 ? 1.0 / (double)(b * b * (b - 1)) : 0.0;
     if (wave == 0) {
-      const double o = pb_score([](int k) { return k; }, S, ld, a, b, inva, invb, lane);
+      const double o = pb_score([](int k) { return k; }, S, ld, a, b, inva, invb, lane, s_fl, s_ls, s_ls + a);
       if (lane == 0) s_obs = o;
     }
     if (tid == 0) {
@@ -1383,7 +1412,8 @@ __global__ void __launch_bounds__(256)
       }
       /* 3. scores: wave v takes tracks v, v + 4, ... */
       for (int q = wave; q < P; q += NT / 64) {
-        const double sc = pb_score([&](int k) { return (int)s_sig[k * P + q]; }, S, ld, a, b, inva, invb, lane);
+        const double sc = pb_score([&](int k) { return (int)s_sig[k * P + q]; }, S, ld, a, b, inva, invb, lane,
+                                   s_fl, s_ls, s_ls + a);
         if (lane == 0) s_hitq[q] = sc >= obs;
       }
       __syncthreads();

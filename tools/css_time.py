@@ -41,5 +41,13 @@ dt = (time.perf_counter() - t) / steps
 print(f"CSS {nch}x{nsnp} {a}+{b} runs={runs}: {nwin} windows, {dt*1e3:.2f} ms/step, {nwin/dt/1e6:.2f} M windows/s, stages {_lib.last_stage_ms()}")
 s = sc.cpu().numpy(); print("computed", (s != 0).sum(), "nan", np.isnan(s).sum(), "mean p", pv.cpu().numpy()[s != 0].mean())
 import json
-print(json.dumps({"css_time": True, "nch": nch, "nsnp": nsnp, "pop": a, "runs": runs, "treshold": tres,
+# mean SNP rows per window of the 2500 / 500 grid (the distance build's npos)
+npw = []
+for c in range(nch):
+    pos = ap[c * alen:(c + 1) * alen:a].cpu().numpy()
+    st0 = np.arange(0, int(last[c]) + 1, 500)
+    k = np.searchsorted(pos, st0 + 2500) - np.searchsorted(pos, st0)
+    npw.append(k[k > 0])
+npos_mean = float(np.concatenate(npw).mean())
+print(json.dumps({"css_time": True, "npos_mean": npos_mean, "nch": nch, "nsnp": nsnp, "pop": a, "runs": runs, "treshold": tres,
                   "windows_per_scan": int(nwin), "scans": steps + 1, "ms_per_step": dt * 1e3}))

@@ -144,7 +144,7 @@ def css_entry(key, d, kernels, windows, what):
 
 
 c3b = last_json(src / "pmc_c3.json")
-css_entry("c3", src / "pmc_c3", ["k_css_pack", "k_css_mds_p40"], c3b["css"]["config"]["windows_per_gpu"],
+css_entry("c3", src / "pmc_c3", ["k_css_pack", "k_css_mds_p40"], c3b["css"]["c3"]["windows_per_gpu"],
           "bench.py C3 leg: 20 x 500k SNPs, 20+20, runs=0")
 c4t = last_json(src / "pmc_c4.txt")
 css_entry("c4", src / "pmc_c4", ["k_css_pack", "k_css_mds_t80"], c4t["windows_per_scan"],
@@ -168,17 +168,46 @@ if (src / "pmc_c5_mfma").exists():
                   "k_css_perm<80> (tools/css_time.py C5 shape); frac = busy / (1024 SIMDs x GRBM_GUI_ACTIVE / 8)"}
 (dst / f"{R}_css_valu.json").write_text(json.dumps(css_doc, indent=1) + "\n")
 
+# ---- CSS distance build: k_css_pack's share of pack + MDS from the kernel traces
+# of the C3 / C4 shapes, the popcount D build's share of the MDS kernel from the GD_CSS_PROFILE
+# phase cycles (tools/ab/cssprof), the shapes' mean SNP rows per window
+phase_doc = {}
+PH = ("D", "fill+center", "tridiag", "bisect", "invit", "back", "score")
+for key, mds in (("c3", "k_css_mds_p40"), ("c4", "k_css_mds_t80")):
+    if not (src / f"kt_{key}").exists() or not (src / f"ph_{key}.err").exists():
+        continue
+    kavg = {short(r["Name"]): float(r["AverageNs"]) for r in csv.DictReader(open(find(src / f"kt_{key}", "kernel_stats.csv")))}
+    if "k_css_pack" not in kavg or mds not in kavg:
+        raise SystemExit(f"kt_{key}: k_css_pack / {mds} absent (have {sorted(kavg)})")
+    lines_ph = [ln for ln in (src / f"ph_{key}.err").read_text().splitlines() if ln.startswith("css-prof cycles:")]
+    if not lines_ph:
+        raise SystemExit(f"ph_{key}.err: no css-prof line (was the cssprof variant loaded?)")
+    vals = [int(t) for t in lines_ph[-1].split(":", 1)[1].split() if t.isdigit()]
+    cyc = dict(zip(PH, vals))
+    tot = sum(cyc.values())
+    t = last_json(src / f"kt_{key}.txt")
+    phase_doc[key] = {
+        "pack_us": kavg["k_css_pack"] / 1e3, "mds_us": kavg[mds] / 1e3,
+        "pack_share": kavg["k_css_pack"] / (kavg["k_css_pack"] + kavg[mds]),
+        "d_share": cyc["D"] / tot, "phase_cycles": cyc, "npos_mean": t["npos_mean"],
+        "windows_per_scan": t["windows_per_scan"],
+        "method": f"tools/css_time.py ({t['nch']} x {t['nsnp']} SNPs, {t['pop']}+{t['pop']}, runs 0): k_css_pack and "
+                  f"{mds} average durations (rocprofv3 --kernel-trace --stats); D share = the phase-0 cycles "
+                  "(regularity check + popcount compare_all) over all phases of the GD_CSS_PROFILE build"}
+if phase_doc:
+    (dst / f"{R}_css_phases.json").write_text(json.dumps(phase_doc, indent=1) + "\n")
+
 # ---- summary
 rows = list(csv.DictReader(open(stats)))
 lines = [f"# {R} profile summary", "",
-         "Commands: tools/profile_r03.sh (bench line; `rocprofv3 --kernel-trace --stats -- python3 bench.py --steps 5 "
+         "Commands: tools/profile_round.sh (bench line; `rocprofv3 --kernel-trace --stats -- python3 bench.py --steps 5 "
          "--warmup 1 --no-cpu --c45-steps 1`; PMC passes in runs of their own).", "",
          "| kernel | calls | avg us | total ms |", "|---|---|---|---|"]
 for r in rows:
     lines.append(f"| {short(r['Name'])} | {r['Calls']} | {float(r['AverageNs']) / 1e3:.1f} | "
                  f"{float(r['TotalDurationNs']) / 1e6:.2f} |")
 alg = bench["roofline"]["alg_bytes_per_step"]
-scan_ms = bench["roofline"]["stage_ms"]["scan_total"]
+scan_ms = bench["stage_ms"]["scan_total"]
 lines += ["", f"VALU issue peak (ubench, median of simple ops): {peak:.0f} G wave-instructions/s "
           f"= {256 * 4 * 2.4 / peak:.2f} cycles per wave64 instruction per SIMD at 2.4 GHz. Per op: "
           + ", ".join(f"{k} {v:.0f}" for k, v in ginst.items()) + ".",
@@ -193,6 +222,10 @@ for k, v in css_doc.items():
                  f"({' + '.join(v['kernels'])})."
                  + (f" Matrix cores: {v['mfma']['mfma_per_dispatch'] / 1e6:.1f} M v_mfma_f32_32x32x16_f16 per "
                     f"dispatch, {100 * v['mfma']['frac']:.1f} % of the SIMD-cycles busy." if "mfma" in v else ""))
+for k, v in phase_doc.items():
+    lines.append(f"CSS {k} distance build: k_css_pack {v['pack_us']:.1f} us + popcount D "
+                 f"{100 * v['d_share']:.1f} % of the MDS kernel ({v['mds_us']:.1f} us), "
+                 f"{v['npos_mean']:.1f} SNP rows per window.")
 lines += ["", "Bench line (same call):", "", "```", json.dumps(bench), "```"]
 (dst / f"{R}_summary.md").write_text("\n".join(lines) + "\n")
 print("\n".join(lines[:60]))

@@ -11,6 +11,8 @@ __global__ void k(unsigned *out, unsigned seed) {
   unsigned long long u[CH];
   const unsigned c = seed * 0x9E3779B9u | 1u;
   const double cd = 1.0000001;
+  const unsigned c2 = c ^ 0x5A5A5A5Au;
+  const unsigned long long sm = 0x5555555555555555ull ^ seed;
   for (int i = 0; i < CH; ++i) { a[i] = seed + threadIdx.x * 7 + i; d[i] = a[i]; u[i] = a[i]; }
   for (int it = 0; it < N_IT; ++it) {
 #pragma unroll
@@ -45,6 +47,32 @@ __global__ void k(unsigned *out, unsigned seed) {
       if (OP == 27) asm volatile("v_mul_f32 %0, %0, %1" : "+v"(a[i]) : "v"(c));
       if (OP == 28) asm volatile("v_pk_mul_f32 %0, %0, %1" : "+v"(u[i]) : "v"(u[0]));
       if (OP == 29) asm volatile("v_mul_lo_u32 %0, %0, %1" : "+v"(a[i]) : "s"(c));
+      if (OP == 30) asm volatile("v_med3_f32 %0, %0, %1, %2" : "+v"(a[i]) : "v"(c), "v"(c2));
+      if (OP == 31) asm volatile("v_max_f32 %0, %0, %1" : "+v"(a[i]) : "v"(c));
+      if (OP == 32) asm volatile("v_min_f32 %0, %0, %1" : "+v"(a[i]) : "v"(c));
+      if (OP == 33) asm volatile("v_max3_f32 %0, %0, %1, %2" : "+v"(a[i]) : "v"(c), "v"(c2));
+      if (OP == 34) asm volatile("v_add_f32 %0, %0, %1" : "+v"(a[i]) : "v"(c));
+      if (OP == 35) asm volatile("v_fma_f32 %0, %0, %1, %2" : "+v"(a[i]) : "v"(c), "v"(c2));
+      if (OP == 36) asm volatile("v_lshlrev_b32 %0, 1, %0" : "+v"(a[i]));
+      if (OP == 37) asm volatile("v_or_b32 %0, %0, %1" : "+v"(a[i]) : "v"(c));
+      if (OP == 38) asm volatile("v_xor_b32 %0, %0, %1" : "+v"(a[i]) : "v"(c));
+      if (OP == 39) asm volatile("v_bfi_b32 %0, %1, %0, %2" : "+v"(a[i]) : "v"(c), "v"(c2));
+      if (OP == 40) asm volatile("v_cndmask_b32_e64 %0, %0, %1, %2" : "+v"(a[i]) : "v"(c), "s"(sm));
+      if (OP == 41) asm volatile("v_max_u32 %0, %0, %1" : "+v"(a[i]) : "v"(c));
+      if (OP == 42) asm volatile("v_min_u32 %0, %0, %1" : "+v"(a[i]) : "v"(c));
+      if (OP == 43) asm volatile("v_max_f64 %0, %0, %1" : "+v"(d[i]) : "v"(cd));
+      if (OP == 44) asm volatile("v_add_f64 %0, %0, %1" : "+v"(d[i]) : "v"(cd));
+      if (OP == 45) asm volatile("v_mov_b32_dpp %0, %1 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf" : "=v"(a[i]) : "v"(a[(i + 1) % CH]));
+      if (OP == 46) asm volatile("v_perm_b32 %0, %0, %1, %2" : "+v"(a[i]) : "v"(c), "v"(c2));
+      if (OP == 47) asm volatile("v_add_co_u32 %0, vcc, %0, %1" : "+v"(a[i]) : "v"(c) : "vcc");
+      if (OP == 48) asm volatile("v_mad_u32_u16 %0, %0, %1, %2" : "+v"(a[i]) : "v"(c), "v"(c2));
+      if (OP == 49) asm volatile("v_pk_max_u16 %0, %0, %1" : "+v"(a[i]) : "v"(c));
+      if (OP == 50) asm volatile("v_pk_add_u16 %0, %0, %1" : "+v"(a[i]) : "v"(c));
+      if (OP == 51) asm volatile("v_add_u16 %0, %0, %1" : "+v"(a[i]) : "v"(c));
+      if (OP == 52) asm volatile("v_cmp_gt_u32 vcc, %0, %1" :: "v"(a[i]), "v"(c) : "vcc");
+      if (OP == 53) asm volatile("v_mul_u32_u24_e32 %0, %0, %1" : "+v"(a[i]) : "v"(c));
+      if (OP == 54) asm volatile("v_mul_hi_u32 %0, %0, %1" : "+v"(a[i]) : "v"(c2));
+      if (OP == 55) asm volatile("v_max_i16 %0, %0, %1" : "+v"(a[i]) : "v"(c));
     }
   }
   unsigned s = 0;
@@ -99,5 +127,31 @@ int main() {
   printf("v_mul_f32        %.1f\n", run<27>(o));
   printf("v_pk_mul_f32     %.1f\n", run<28>(o));
   printf("v_mul_lo_u32 s   %.1f\n", run<29>(o));
+  printf("v_med3_f32       %.1f\n", run<30>(o));
+  printf("v_max_f32        %.1f\n", run<31>(o));
+  printf("v_min_f32        %.1f\n", run<32>(o));
+  printf("v_max3_f32       %.1f\n", run<33>(o));
+  printf("v_add_f32        %.1f\n", run<34>(o));
+  printf("v_fma_f32        %.1f\n", run<35>(o));
+  printf("v_lshlrev_b32    %.1f\n", run<36>(o));
+  printf("v_or_b32         %.1f\n", run<37>(o));
+  printf("v_xor_b32        %.1f\n", run<38>(o));
+  printf("v_bfi_b32        %.1f\n", run<39>(o));
+  printf("v_cndmask_b32 sgpr%.1f\n", run<40>(o));
+  printf("v_max_u32        %.1f\n", run<41>(o));
+  printf("v_min_u32        %.1f\n", run<42>(o));
+  printf("v_max_f64        %.1f\n", run<43>(o));
+  printf("v_add_f64        %.1f\n", run<44>(o));
+  printf("v_mov_b32_dpp    %.1f\n", run<45>(o));
+  printf("v_perm_b32       %.1f\n", run<46>(o));
+  printf("v_add_co_u32     %.1f\n", run<47>(o));
+  printf("v_mad_u32_u16    %.1f\n", run<48>(o));
+  printf("v_pk_max_u16     %.1f\n", run<49>(o));
+  printf("v_pk_add_u16     %.1f\n", run<50>(o));
+  printf("v_add_u16        %.1f\n", run<51>(o));
+  printf("v_cmp_gt_u32     %.1f\n", run<52>(o));
+  printf("v_mul_u32_u24 e32%.1f\n", run<53>(o));
+  printf("v_mul_hi_u32 x2  %.1f\n", run<54>(o));
+  printf("v_max_i16        %.1f\n", run<55>(o));
   return 0;
 }
