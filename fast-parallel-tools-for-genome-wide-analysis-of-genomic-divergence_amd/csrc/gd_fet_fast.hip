@@ -112,12 +112,37 @@ __device__ __forceinline__ int fmod_n(uint32_t r, uint32_t magic, uint32_t shift
 
 /* one LCG step on the 32-bit halves of y: lo*a_lo + c16 as one v_mad_u64_u32,
  * the high word gets hi*a_lo (v_mul_lo_u32) and lo*5 (a's high part; v_lshl_add) */
+#ifndef FW_LCG_MAD
+#define FW_LCG_MAD 1
+#endif
+#if FW_LCG_MAD
+/* The same step as two v_mad_u64_u32 and one v_mad_u32_u24 (+ a shift): ylo's low 16 bits
+ * are 0 (y = x << 16), so 5 ylo + hi(t) = (ylo >> 16) (5 << 16) + hi(t) is a 24-bit
+ * multiply-add, and a_lo yhi + that is the low word of one v_mad_u64_u32 whose addend is
+ * a fresh register pair (its high word is don't-care: only the low word of the result is used).
+ * 14 issue cycles per step against 16 (ubench: the multiplies and VOP3 adds are 4-cycle
+ * instructions, the shift 2). */
+#define FW_STEP()                                                                          \
+  do {                                                                                     \
+    const uint64_t t_ = (uint64_t)ylo * 0xDEECE66Du + FW_C16;                              \
+    const uint32_t s_ = __umul24(ylo >> 16, 5u << 16) + (uint32_t)(t_ >> 32);             \
+    uint64_t acc_;                                                                         \
+    asm volatile("" : "=v"(acc_)); /* a fresh pair, high word undefined */             \
+    acc_ = (acc_ & 0xFFFFFFFF00000000ull) | s_;                                            \
+    asm("v_mad_u64_u32 %0, vcc, %1, %2, %0" : "+v"(acc_) : "v"(yhi), "s"(a_lo) : "vcc");  \
+    yhi = (uint32_t)acc_;                                                                  \
+    ylo = (uint32_t)t_;                                                                    \
+  } while (0)
+#define FW_LCG_DECL const uint32_t a_lo = __builtin_amdgcn_readfirstlane(0xDEECE66Du)
+#else
 #define FW_STEP()                                                              \
   do {                                                                         \
     const uint64_t t_ = (uint64_t)ylo * 0xDEECE66Du + FW_C16;                  \
     yhi = (uint32_t)(t_ >> 32) + yhi * 0xDEECE66Du + ylo * 5u;                 \
     ylo = (uint32_t)t_;                                                        \
   } while (0)
+#define FW_LCG_DECL
+#endif
 
 /* Order key of a draw without the remainder.  The draw is r = yhi >> 1 and the
  * sampled index r mod n; yhi = 2r + (yhi & 1) gives yhi mod 2n = 2 (r mod n) + bit,
@@ -163,6 +188,7 @@ __device__ __forceinline__ void draw_rep(uint32_t &ylo, uint32_t &yhi, uint32_t 
                                          uint32_t mlo, uint32_t mhi, uint32_t &ymax) {
 #pragma unroll
   for (int i = 0; i < MT; ++i) K[i] = 0u;
+  FW_LCG_DECL;
   int j = 0;
   for (; j < lo8; j += 8) {
     FW_DRAW(MT);
@@ -531,7 +557,14 @@ __device__ __forceinline__ void fw_clean8(double (&v)[8]) {
 #undef FW_CX2
 }
 
-__global__ void __launch_bounds__(FW_WPB *FW_TPW)
+/* register-allocation target: 7 waves per SIMD (the LDS limit of 7 workgroups per CU); left
+ * to itself the allocator takes 76 VGPRs (6 waves) for the FW_LCG_MAD step, and 7 waves ran
+ * 0.7-1 % faster (C2: 2.365-2.380 against 2.383-2.385 ms/step; FW_LCG_MAD=0: 2.397-2.412) */
+#ifndef FW_WAVES_PER_SIMD
+#define FW_WAVES_PER_SIMD 7
+#endif
+#define FW_WPE __attribute__((amdgpu_waves_per_eu(FW_WAVES_PER_SIMD, 8)))
+__global__ void __launch_bounds__(FW_WPB *FW_TPW) FW_WPE
     k_fet_window_fast(const gd_chrom_dev *ch, int nchrom, const int32_t *blk_off, int blk_base,
                       const int32_t *lo_a, const int32_t *hi_a, const int32_t *lo_b, const double *snp_score,
                       const double *avals, const double *bvals, const uint64_t *binom, const int *lut_hdr,
