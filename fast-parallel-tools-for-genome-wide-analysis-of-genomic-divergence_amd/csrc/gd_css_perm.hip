@@ -419,8 +419,7 @@ __device__ __forceinline__ void score_mfma(const char *s16, const uint2 *lut, co
   float wa = 0.f, wb = 0.f;
   uint32_t prev = 0;
   constexpr int CK = 16; /* rows m .. MP - 1 of the byte matrix hold 0 (sig_identity) */
-#pragma unroll
-  for (int k0 = 0; k0 < MP; k0 += CK) {
+  auto batch = [&](int k0) {
     if (k0 < m) {
       uint32_t c[CK];
 #pragma unroll
@@ -441,6 +440,19 @@ __device__ __forceinline__ void score_mfma(const char *s16, const uint2 *lut, co
       }
       prev = c[CK - 1];
     }
+  };
+  /* Above 64 individuals the batches run as a loop: unrolled, the compiler hoisted every
+   * (k < a), (k > a), (k < m) test of the MP entries out of the permutation loop as SGPR
+   * masks and spilled them to VGPR lanes (467 SGPR spills at 80, a v_readlane per use);
+   * rolled, the tests are scalar compares in the loop (C5 shape 8.40-8.43 -> 8.07-8.16 ms per
+   * 50k windows).  At 40 the unrolled form stays ahead (20+20 with mcR 1000: 15.86 against
+   * 16.06 ms per 200k windows). */
+  if constexpr (MP > 64) {
+#pragma unroll 1
+    for (int k0 = 0; k0 < MP; k0 += CK) batch(k0);
+  } else {
+#pragma unroll
+    for (int k0 = 0; k0 < MP; k0 += CK) batch(k0);
   }
   hi = hi32;
   const uint64_t vlo = m >= 64 ? ~0ull : ((1ull << m) - 1), vhi = m > 64 ? ((1ull << (m - 64)) - 1) : 0ull;
@@ -566,9 +578,45 @@ __device__ __forceinline__ uint32_t perm_mag(uint32_t vm0, uint32_t vm1, int n) 
   return n < 64 ? lo : hi;
 }
 
+/* One nrand48 step on y = x << 16 (mod 2^64), as the FET draw loop takes it (gd_fet_fast.hip
+ * FW_STEP): ylo's low 16 bits are 0, so the high word a_lo yhi + 5 ylo + hi(a_lo ylo + c16)
+ * is one v_mad_u64_u32 whose addend 5 ylo + hi(...) is a v_mad_u32_u24 of ylo >> 16
+ * (14 issue cycles against 16 for the compiler's mul_lo / lshl_add / add3 form) */
+#ifndef PERM_LCG_MAD
+#define PERM_LCG_MAD 0 /* measured neutral to slower here (C5 shape) */
+#endif
+__device__ __forceinline__ void perm_lcg_step(uint64_t &y) {
+#if PERM_LCG_MAD
+  const uint32_t ylo = (uint32_t)y, yhi = (uint32_t)(y >> 32);
+  const uint64_t t = (uint64_t)ylo * 0xDEECE66Du + (GD_LCG_C << 16);
+  const uint32_t s = __umul24(ylo >> 16, 5u << 16) + (uint32_t)(t >> 32);
+  uint64_t acc;
+  asm volatile("" : "=v"(acc)); /* a fresh pair: its high word is don't-care */
+  acc = (acc & 0xFFFFFFFF00000000ull) | s;
+  asm("v_mad_u64_u32 %0, vcc, %1, %2, %0" : "+v"(acc) : "v"(yhi), "s"(0xDEECE66Du) : "vcc");
+  y = ((uint64_t)(uint32_t)acc << 32) | (uint32_t)t;
+#else
+  y = y * GD_LCG_A + (GD_LCG_C << 16);
+#endif
+}
+
+/* Rejection tracking by the largest draw (1) or by each step's own limit (0, the default:
+ * with the running maximum the straight-line Fisher-Yates held more draws in flight, 171
+ * VGPRs at 80, and the C5 shape ran 8.54 against 8.08-8.10 ms per 50k windows) */
+#ifndef PERM_RMAX
+#define PERM_RMAX 0
+#endif
+/* A draw r of step n is rejected iff r > RAND_MAX - 2^31 mod n >= 2^31 - n, so no draw of a
+ * permutation of m individuals is rejected unless its largest draw exceeds 2^31 - 1 - m: one
+ * v_max per step instead of a compare against each step's own limit (probability of the
+ * conservative flag ~ 64 (m - 1) m / 2^31 per pass, ~2e-4 at 80; a flagged pass takes the
+ * exact serial stream, which applies the real limits).  With PERM_RMAX = 0 the steps keep
+ * all-ones in rmax when their own limit rejects, which this test also reads. */
+__device__ __forceinline__ bool fy_rej_possible(uint32_t rmax, int m) { return rmax > 0x7FFFFFFFu - (uint32_t)m; }
+
 /* Fisher-Yates swaps of random_shuffle (css.c:700-706) on the lane's column, draws
- * from state x (no rejection: the caller checks); returns true if a draw would have
- * been rejected.
+ * from state x (no rejection: the caller checks); returns true if a draw may have
+ * been rejected (the caller then redraws from the exact serial stream).
  *
  * Software-pipelined: step n swaps positions n - 1 and j_n.  The two reads of step
  * n - 1 are issued before the two writes of step n (LDS is in order per wave, so they
@@ -635,12 +683,18 @@ __device__ __forceinline__ bool fy_fast(uint8_t *col, uint64_t x, int m, uint32_
     *at(j) = u;
   }
 #else
-  /* steps n >= 64 read their magic from vm1, the rest from vm0: one readlane per step */
+  /* steps n >= 64 read their magic from vm1, the rest from vm0: one readlane per step.
+   * Rejections by the largest draw (fy_rej_possible) */
+  uint32_t rmax = 0;
   auto step = [&](int n, uint32_t mg) {
     const gd_randint rd = perm_rd((uint32_t)n, mg);
-    y = y * GD_LCG_A + (GD_LCG_C << 16);
+    perm_lcg_step(y);
     const uint32_t r = (uint32_t)(y >> 33);
-    rej |= r > rd.limit;
+#if PERM_RMAX
+    rmax = max(rmax, r);
+#else
+    rmax |= r > rd.limit ? 0xFFFFFFFFu : 0u;
+#endif
     const uint32_t j = r - (__umulhi(r, rd.magic) >> rd.shift) * (uint32_t)n;
     const uint8_t u = *at((uint32_t)(n - 1)), v = *at(j);
     *at((uint32_t)(n - 1)) = v;
@@ -649,6 +703,7 @@ __device__ __forceinline__ bool fy_fast(uint8_t *col, uint64_t x, int m, uint32_
   int n = __builtin_amdgcn_readfirstlane(m);
   for (; n >= 64; --n) step(n, (uint32_t)__builtin_amdgcn_readlane((int)vm1, n - 64));
   for (; n >= 2; --n) step(n, (uint32_t)__builtin_amdgcn_readlane((int)vm0, n));
+  rej = fy_rej_possible(rmax, m);
 #endif
   return rej;
 }
@@ -674,11 +729,15 @@ constexpr PmRd pm_rd_const(uint32_t n) {
  * arithmetic.  Taken when the window fills its tier (m == MP, e.g. 40 + 40); other
  * cohorts run the loop (fy_fast). */
 template <int N>
-__device__ __forceinline__ void fy_step(uint8_t *col, uint64_t &y, bool &rej) {
+__device__ __forceinline__ void fy_step(uint8_t *col, uint64_t &y, uint32_t &rmax) {
   constexpr PmRd rd = pm_rd_const((uint32_t)N);
-  y = y * GD_LCG_A + (GD_LCG_C << 16);
+  perm_lcg_step(y);
   const uint32_t r = (uint32_t)(y >> 33);
-  rej |= r > rd.limit;
+#if PERM_RMAX
+  rmax = max(rmax, r);
+#else
+  rmax |= r > rd.limit ? 0xFFFFFFFFu : 0u;
+#endif
   const uint32_t j = r - (__umulhi(r, rd.magic) >> rd.shift) * (uint32_t)N;
   uint8_t *pn = col + (N - 1) * PERM_ROW;
   uint8_t *pj = col + __umul24(j, (uint32_t)PERM_ROW);
@@ -687,19 +746,19 @@ __device__ __forceinline__ void fy_step(uint8_t *col, uint64_t &y, bool &rej) {
   *pj = u;
 }
 template <int N>
-__device__ __forceinline__ void fy_steps(uint8_t *col, uint64_t &y, bool &rej) {
+__device__ __forceinline__ void fy_steps(uint8_t *col, uint64_t &y, uint32_t &rmax) {
   if constexpr (N >= 2) {
-    fy_step<N>(col, y, rej);
-    fy_steps<N - 1>(col, y, rej);
+    fy_step<N>(col, y, rmax);
+    fy_steps<N - 1>(col, y, rmax);
   }
 }
 /* a full tier (m == MP): the steps n = MP .. 2 as one straight line */
 template <int MP>
 __device__ __forceinline__ bool fy_fast_unrolled(uint8_t *col, uint64_t x) {
-  bool rej = false;
+  uint32_t rmax = 0;
   uint64_t y = x << 16;
-  fy_steps<MP>(col, y, rej);
-  return rej;
+  fy_steps<MP>(col, y, rmax);
+  return fy_rej_possible(rmax, MP);
 }
 
 /* the same with random_int_nrand48's redraw loop (css.c:675-690) */
@@ -1215,23 +1274,27 @@ template <int MP>
 constexpr int pb_p() { return MP > 512 ? 32 : 64; }
 
 /* Fisher-Yates of random_shuffle (css.c:700-706) on column `col` (stride PB_P), draws
- * from state x without rejection; true if a draw would have been rejected */
+ * from state x without rejection; true if a draw may have been rejected */
 template <int PB_P>
 __device__ __forceinline__ bool fy_big_fast(uint16_t *col, uint64_t x, int m, const uint32_t *mag) {
-  bool rej = false;
+  uint32_t rmax = 0;
   uint64_t y = x << 16;
   for (int s = 0; s < m - 1; ++s) {
     const int n = __builtin_amdgcn_readfirstlane(m - s);
     const gd_randint rd = perm_rd((uint32_t)n, __builtin_amdgcn_readfirstlane(mag[n]));
     y = y * GD_LCG_A + (GD_LCG_C << 16);
     const uint32_t r = (uint32_t)(y >> 33);
-    rej |= r > rd.limit;
+#if PERM_RMAX
+    rmax = max(rmax, r);
+#else
+    rmax |= r > rd.limit ? 0xFFFFFFFFu : 0u;
+#endif
     const int j = (int)(r - (__umulhi(r, rd.magic) >> rd.shift) * (uint32_t)n);
     const uint16_t u = col[(n - 1) * PB_P], v = col[j * PB_P];
     col[(n - 1) * PB_P] = v;
     col[j * PB_P] = u;
   }
-  return rej;
+  return fy_rej_possible(rmax, m);
 }
 
 /* the same with random_int_nrand48's redraw loop (css.c:675-690) */
