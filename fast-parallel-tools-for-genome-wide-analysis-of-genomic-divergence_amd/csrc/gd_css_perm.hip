@@ -600,23 +600,16 @@ __device__ __forceinline__ void perm_lcg_step(uint64_t &y) {
 #endif
 }
 
-/* Rejection tracking by the largest draw (1) or by each step's own limit (0, the default:
- * with the running maximum the straight-line Fisher-Yates held more draws in flight, 171
- * VGPRs at 80, and the C5 shape ran 8.54 against 8.08-8.10 ms per 50k windows) */
-#ifndef PERM_RMAX
-#define PERM_RMAX 0
+/* the draw of a straight-line step as an opaque 32-bit value (PERM_R_FENCE): otherwise the
+ * compiler folds (y >> 33) > limit into a 64-bit compare of y against a per-step 64-bit
+ * constant, hoists the 2 (MP - 1) constant words out of the permutation loop and spills them
+ * (80: 187 -> 71 SGPR spills) */
+#ifndef PERM_R_FENCE
+#define PERM_R_FENCE 1
 #endif
-/* A draw r of step n is rejected iff r > RAND_MAX - 2^31 mod n >= 2^31 - n, so no draw of a
- * permutation of m individuals is rejected unless its largest draw exceeds 2^31 - 1 - m: one
- * v_max per step instead of a compare against each step's own limit (probability of the
- * conservative flag ~ 64 (m - 1) m / 2^31 per pass, ~2e-4 at 80; a flagged pass takes the
- * exact serial stream, which applies the real limits).  With PERM_RMAX = 0 the steps keep
- * all-ones in rmax when their own limit rejects, which this test also reads. */
-__device__ __forceinline__ bool fy_rej_possible(uint32_t rmax, int m) { return rmax > 0x7FFFFFFFu - (uint32_t)m; }
-
 /* Fisher-Yates swaps of random_shuffle (css.c:700-706) on the lane's column, draws
- * from state x (no rejection: the caller checks); returns true if a draw may have
- * been rejected (the caller then redraws from the exact serial stream).
+ * from state x (no rejection: the caller checks); returns true if a draw would have
+ * been rejected.
  *
  * Software-pipelined: step n swaps positions n - 1 and j_n.  The two reads of step
  * n - 1 are issued before the two writes of step n (LDS is in order per wave, so they
@@ -683,18 +676,12 @@ __device__ __forceinline__ bool fy_fast(uint8_t *col, uint64_t x, int m, uint32_
     *at(j) = u;
   }
 #else
-  /* steps n >= 64 read their magic from vm1, the rest from vm0: one readlane per step.
-   * Rejections by the largest draw (fy_rej_possible) */
-  uint32_t rmax = 0;
+  /* steps n >= 64 read their magic from vm1, the rest from vm0: one readlane per step */
   auto step = [&](int n, uint32_t mg) {
     const gd_randint rd = perm_rd((uint32_t)n, mg);
     perm_lcg_step(y);
     const uint32_t r = (uint32_t)(y >> 33);
-#if PERM_RMAX
-    rmax = max(rmax, r);
-#else
-    rmax |= r > rd.limit ? 0xFFFFFFFFu : 0u;
-#endif
+    rej |= r > rd.limit;
     const uint32_t j = r - (__umulhi(r, rd.magic) >> rd.shift) * (uint32_t)n;
     const uint8_t u = *at((uint32_t)(n - 1)), v = *at(j);
     *at((uint32_t)(n - 1)) = v;
@@ -703,7 +690,6 @@ __device__ __forceinline__ bool fy_fast(uint8_t *col, uint64_t x, int m, uint32_
   int n = __builtin_amdgcn_readfirstlane(m);
   for (; n >= 64; --n) step(n, (uint32_t)__builtin_amdgcn_readlane((int)vm1, n - 64));
   for (; n >= 2; --n) step(n, (uint32_t)__builtin_amdgcn_readlane((int)vm0, n));
-  rej = fy_rej_possible(rmax, m);
 #endif
   return rej;
 }
@@ -728,16 +714,13 @@ constexpr PmRd pm_rd_const(uint32_t n) {
  * the LCG, the remainder, one address and the swap -- no readlane, no scalar
  * arithmetic.  Taken when the window fills its tier (m == MP, e.g. 40 + 40); other
  * cohorts run the loop (fy_fast). */
-template <int N>
-__device__ __forceinline__ void fy_step(uint8_t *col, uint64_t &y, uint32_t &rmax) {
+template <int N, bool FENCE>
+__device__ __forceinline__ void fy_step(uint8_t *col, uint64_t &y, bool &rej) {
   constexpr PmRd rd = pm_rd_const((uint32_t)N);
   perm_lcg_step(y);
-  const uint32_t r = (uint32_t)(y >> 33);
-#if PERM_RMAX
-  rmax = max(rmax, r);
-#else
-  rmax |= r > rd.limit ? 0xFFFFFFFFu : 0u;
-#endif
+  uint32_t r = (uint32_t)(y >> 33);
+  if constexpr (FENCE) asm("" : "+v"(r));
+  rej |= r > rd.limit;
   const uint32_t j = r - (__umulhi(r, rd.magic) >> rd.shift) * (uint32_t)N;
   uint8_t *pn = col + (N - 1) * PERM_ROW;
   uint8_t *pj = col + __umul24(j, (uint32_t)PERM_ROW);
@@ -745,20 +728,20 @@ __device__ __forceinline__ void fy_step(uint8_t *col, uint64_t &y, uint32_t &rma
   *pn = v;
   *pj = u;
 }
-template <int N>
-__device__ __forceinline__ void fy_steps(uint8_t *col, uint64_t &y, uint32_t &rmax) {
+template <int N, bool FENCE>
+__device__ __forceinline__ void fy_steps(uint8_t *col, uint64_t &y, bool &rej) {
   if constexpr (N >= 2) {
-    fy_step<N>(col, y, rmax);
-    fy_steps<N - 1>(col, y, rmax);
+    fy_step<N, FENCE>(col, y, rej);
+    fy_steps<N - 1, FENCE>(col, y, rej);
   }
 }
 /* a full tier (m == MP): the steps n = MP .. 2 as one straight line */
 template <int MP>
 __device__ __forceinline__ bool fy_fast_unrolled(uint8_t *col, uint64_t x) {
-  uint32_t rmax = 0;
+  bool rej = false;
   uint64_t y = x << 16;
-  fy_steps<MP>(col, y, rmax);
-  return fy_rej_possible(rmax, MP);
+  fy_steps<MP, (PERM_R_FENCE != 0) && MP <= 80>(col, y, rej); /* at 96 the fence cost registers: 2 -> 1 wave */
+  return rej;
 }
 
 /* the same with random_int_nrand48's redraw loop (css.c:675-690) */
@@ -1274,27 +1257,23 @@ template <int MP>
 constexpr int pb_p() { return MP > 512 ? 32 : 64; }
 
 /* Fisher-Yates of random_shuffle (css.c:700-706) on column `col` (stride PB_P), draws
- * from state x without rejection; true if a draw may have been rejected */
+ * from state x without rejection; true if a draw would have been rejected */
 template <int PB_P>
 __device__ __forceinline__ bool fy_big_fast(uint16_t *col, uint64_t x, int m, const uint32_t *mag) {
-  uint32_t rmax = 0;
+  bool rej = false;
   uint64_t y = x << 16;
   for (int s = 0; s < m - 1; ++s) {
     const int n = __builtin_amdgcn_readfirstlane(m - s);
     const gd_randint rd = perm_rd((uint32_t)n, __builtin_amdgcn_readfirstlane(mag[n]));
     y = y * GD_LCG_A + (GD_LCG_C << 16);
     const uint32_t r = (uint32_t)(y >> 33);
-#if PERM_RMAX
-    rmax = max(rmax, r);
-#else
-    rmax |= r > rd.limit ? 0xFFFFFFFFu : 0u;
-#endif
+    rej |= r > rd.limit;
     const int j = (int)(r - (__umulhi(r, rd.magic) >> rd.shift) * (uint32_t)n);
     const uint16_t u = col[(n - 1) * PB_P], v = col[j * PB_P];
     col[(n - 1) * PB_P] = v;
     col[j * PB_P] = u;
   }
-  return fy_rej_possible(rmax, m);
+  return rej;
 }
 
 /* the same with random_int_nrand48's redraw loop (css.c:675-690) */
