@@ -115,34 +115,35 @@ __device__ __forceinline__ int fmod_n(uint32_t r, uint32_t magic, uint32_t shift
 #ifndef FW_LCG_MAD
 #define FW_LCG_MAD 1
 #endif
-#if FW_LCG_MAD
-/* The same step as two v_mad_u64_u32 and one v_mad_u32_u24 (+ a shift): ylo's low 16 bits
- * are 0 (y = x << 16), so 5 ylo + hi(t) = (ylo >> 16) (5 << 16) + hi(t) is a 24-bit
- * multiply-add, and a_lo yhi + that is the low word of one v_mad_u64_u32 whose addend is
- * a fresh register pair (its high word is don't-care: only the low word of the result is used).
- * 14 issue cycles per step against 16 (ubench: the multiplies and VOP3 adds are 4-cycle
- * instructions, the shift 2). */
-#define FW_STEP()                                                                          \
-  do {                                                                                     \
-    const uint64_t t_ = (uint64_t)ylo * 0xDEECE66Du + FW_C16;                              \
-    const uint32_t s_ = __umul24(ylo >> 16, 5u << 16) + (uint32_t)(t_ >> 32);             \
-    uint64_t acc_;                                                                         \
-    asm volatile("" : "=v"(acc_)); /* a fresh pair, high word undefined */             \
-    acc_ = (acc_ & 0xFFFFFFFF00000000ull) | s_;                                            \
-    asm("v_mad_u64_u32 %0, vcc, %1, %2, %0" : "+v"(acc_) : "v"(yhi), "s"(a_lo) : "vcc");  \
-    yhi = (uint32_t)acc_;                                                                  \
-    ylo = (uint32_t)t_;                                                                    \
-  } while (0)
-#define FW_LCG_DECL const uint32_t a_lo = __builtin_amdgcn_readfirstlane(0xDEECE66Du)
-#else
-#define FW_STEP()                                                              \
-  do {                                                                         \
-    const uint64_t t_ = (uint64_t)ylo * 0xDEECE66Du + FW_C16;                  \
-    yhi = (uint32_t)(t_ >> 32) + yhi * 0xDEECE66Du + ylo * 5u;                 \
-    ylo = (uint32_t)t_;                                                        \
-  } while (0)
-#define FW_LCG_DECL
+/* MAD: the same step as two v_mad_u64_u32 and one v_mad_u32_u24 (+ a shift): ylo's low 16
+ * bits are 0 (y = x << 16), so 5 ylo + hi(t) = (ylo >> 16) (5 << 16) + hi(t) is a 24-bit
+ * multiply-add, and a_lo yhi + that is the low word of one v_mad_u64_u32 whose addend is a
+ * fresh register pair (its high word is don't-care: only the low word of the result is
+ * used).  14 issue cycles per step against 16 (ubench: the multiplies and VOP3 adds are
+ * 4-cycle instructions, the shift 2). */
+template <bool MAD>
+__device__ __forceinline__ void fw_step(uint32_t &ylo, uint32_t &yhi, uint32_t a_lo) {
+  const uint64_t t = (uint64_t)ylo * 0xDEECE66Du + FW_C16;
+  if constexpr (MAD) {
+    const uint32_t s = __umul24(ylo >> 16, 5u << 16) + (uint32_t)(t >> 32);
+    uint64_t acc;
+    asm volatile("" : "=v"(acc)); /* a fresh pair, high word undefined */
+    acc = (acc & 0xFFFFFFFF00000000ull) | s;
+    asm("v_mad_u64_u32 %0, vcc, %1, %2, %0" : "+v"(acc) : "v"(yhi), "s"(a_lo) : "vcc");
+    yhi = (uint32_t)acc;
+  } else {
+    yhi = (uint32_t)(t >> 32) + yhi * 0xDEECE66Du + ylo * 5u;
+  }
+  ylo = (uint32_t)t;
+}
+/* the MAD step where the top list holds at most FW_LCG_MAD_MT keys (4: nearly every wave); in
+ * the MT = 5 / 8 loops its extra registers pushed the 7-wave kernel into scratch (2-4 VGPRs,
+ * ~0.2 GB of scratch traffic per C2 scan) */
+#define FW_STEP() fw_step<FW_LCG_MAD && (MT <= FW_LCG_MAD_MT)>(ylo, yhi, a_lo)
+#ifndef FW_LCG_MAD_MT
+#define FW_LCG_MAD_MT 4
 #endif
+#define FW_LCG_DECL const uint32_t a_lo = __builtin_amdgcn_readfirstlane(0xDEECE66Du)
 
 /* Order key of a draw without the remainder.  The draw is r = yhi >> 1 and the
  * sampled index r mod n; yhi = 2r + (yhi & 1) gives yhi mod 2n = 2 (r mod n) + bit,
