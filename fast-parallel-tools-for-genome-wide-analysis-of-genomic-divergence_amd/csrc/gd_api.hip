@@ -475,8 +475,12 @@ static int fet_scan_locked(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, cons
    * VALU-bound bootstrap of each group on the low-priority stream as soon as the
    * group's rows are scored.  The caller's stream `s` orders the scan against its
    * other work. */
-  hipStream_t sm = ctx->stream_mem, s2 = ctx->stream2;
-  HIP_TRY(hipStreamWaitEvent(sm, ctx->ev[0], 0));
+  int G = std::min(nchrom, GD_DEFAULT_GROUPS);
+  if (const char *eg = getenv("GD_GROUPS")) G = std::max(1, std::min(std::min(nchrom, GD_MAX_GROUPS), atoi(eg))); /* diagnostics */
+  /* one group (the default): every kernel on the caller's stream, no cross-stream event waits
+   * between the passes */
+  hipStream_t sm = G > 1 ? ctx->stream_mem : s, s2 = G > 1 ? ctx->stream2 : s;
+  if (G > 1) HIP_TRY(hipStreamWaitEvent(sm, ctx->ev[0], 0));
   if (!pk) hipLaunchKernelGGL(k_popsize, dim3(nchrom), dim3(64), 0, sm, d_ch, apos, bpos, flags);
   bool force_general = false;
   if ((st = gd_fet_window_prepare(pl.wtotal, list, list_count, sm, &force_general))) return st;
@@ -491,8 +495,6 @@ static int fet_scan_locked(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, cons
    * restores the per-SNP pass feeding the window kernel through snp_score */
   const char *uf = getenv("GD_FET_UNFUSED");
   const bool fused = !pk && !(uf && uf[0] == '1'); /* packed: the per-SNP pass reads 2 bits per genotype */
-  int G = std::min(nchrom, GD_DEFAULT_GROUPS);
-  if (const char *eg = getenv("GD_GROUPS")) G = std::max(1, std::min(std::min(nchrom, GD_MAX_GROUPS), atoi(eg))); /* diagnostics */
   std::vector<int> cuts(G + 1);
   for (int g = 0; g <= G; ++g) cuts[g] = (int)((int64_t)nchrom * g / G);
   for (int g = 0; g < G; ++g) {
@@ -524,15 +526,17 @@ static int fet_scan_locked(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, cons
   HIP_TRY(hipEventRecord(ctx->ev[1], sm));
   for (int g = 0; g < G && !force_general; ++g) {
     const int c0 = cuts[g], c1 = cuts[g + 1];
-    HIP_TRY(hipStreamWaitEvent(s2, ctx->gev[g], 0));
+    if (G > 1) HIP_TRY(hipStreamWaitEvent(s2, ctx->gev[g], 0));
     st = gd_fet_window_fast_launch(d_ch, nchrom, d_blk, blk_off[c0], blk_off[c1] - blk_off[c0], lo_a, hi_a, lo_b,
                                    snp, avals, bvals, binom, ctx->lut_hdr, ctx->lut, fused ? 1 : 0, perc, scores,
                                    stddev, flags, list, list_count, s2);
     if (st) return fail(st, "fast window kernel launch failed");
   }
   HIP_TRY(hipEventRecord(ctx->ev[2], s2));
-  HIP_TRY(hipStreamWaitEvent(s, ctx->ev[1], 0));
-  HIP_TRY(hipStreamWaitEvent(s, ctx->ev[2], 0));
+  if (G > 1) {
+    HIP_TRY(hipStreamWaitEvent(s, ctx->ev[1], 0));
+    HIP_TRY(hipStreamWaitEvent(s, ctx->ev[2], 0));
+  }
   {
     /* windows the fast path declined: literal one-workgroup-per-window path */
     const unsigned gx = (unsigned)std::min<int64_t>(pl.wtotal, 4096);

@@ -160,8 +160,13 @@ def test_device_synth_matches_numpy():
         assert np.array_equal(x.cpu().numpy(), y)
 
 
-def test_device_batch_api_matches_host(oracle):
-    """Several chromosomes in one device scan == per-chromosome scans."""
+@pytest.mark.parametrize("groups", [None, "2", "4"])
+def test_device_batch_api_matches_host(oracle, monkeypatch, groups):
+    """Several chromosomes in one device scan == per-chromosome scans; with GD_GROUPS the
+    scan pipelines chromosome groups over the context's two streams (the default, one
+    group, runs every pass on the caller's stream)."""
+    if groups:
+        monkeypatch.setenv("GD_GROUPS", groups)
     import torch
     from gdscan import _lib, synth
     from gdscan._lib import Chrom, check, lib
