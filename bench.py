@@ -881,6 +881,16 @@ def main():
             roof["valu_issue_peak_ginsts"] = VALU_ISSUE_GINSTS
             roof["valu_frac"] = roof["valu_ginsts"] / VALU_ISSUE_GINSTS
             roof["valu_insts_per_scan"] = vr["valu_wave_insts_per_scan"]
+            if UBENCH_FILE.exists():
+                # the measured issue rate of the 4-cycle instructions the draw loop consists of
+                # (tools/ubench_valu.hip on the box: multiplies and VOP3 three-source ops)
+                ub = json.loads(UBENCH_FILE.read_text()).get("ginsts_per_op", {})
+                ops = [ub[k] for k in ("v_mad_u64_u32", "v_mul_lo_u32", "v_mul_hi_u32", "v_mad_u32_u24",
+                                       "v_med3_i32", "v_max3_u32", "v_add3_u32", "v_lshl_add_u32") if k in ub]
+                if ops:
+                    roof["valu_4cycle_measured_ginsts"] = float(np.median(ops))
+                    roof["valu_frac_4cycle_measured"] = roof["valu_ginsts"] / roof["valu_4cycle_measured_ginsts"]
+                    sources["valu_4cycle"] = f"{UBENCH_FILE.relative_to(ROOT)}: median of {len(ops)} 4-cycle ops"
             if "window_kernel_valu_busy" in vr:
                 roof["window_kernel_valu_busy"] = vr["window_kernel_valu_busy"]
             sources["valu"] = f"{VALU_FILE.relative_to(ROOT)}: {vr['method']}"
