@@ -1607,9 +1607,12 @@ __global__ void __launch_bounds__(64, 2)
     /* ---- compare_all: main row i in A, tail row R's columns 4s + tq into s_tail */
     double A[MP];
     {
-      int acc[MP], acct[T80_TS];
+      /* the main row's counts accumulate in A itself (exact integers in FP64): an int
+       * accumulator array beside A held 80 more VGPRs at the conversion and pushed the
+       * kernel into scratch */
+      int acct[T80_TS];
 #pragma unroll
-      for (int jj = 0; jj < MP; ++jj) acc[jj] = 0;
+      for (int jj = 0; jj < MP; ++jj) A[jj] = 0.0;
 #pragma unroll
       for (int s = 0; s < T80_TS; ++s) acct[s] = 0;
       if (!literal) {
@@ -1634,10 +1637,10 @@ __global__ void __launch_bounds__(64, 2)
           const uint64_t Pi = mk[2 * i], Ni = mk[2 * i + 1];
 #pragma unroll
           for (int jj = 0; jj < MP; ++jj) {
-            acc[jj] += __popcll(Pi & mk[2 * jj + 1]) + __popcll(Ni & mk[2 * jj]);
+            A[jj] += (double)(__popcll(Pi & mk[2 * jj + 1]) + __popcll(Ni & mk[2 * jj]));
             if ((jj & 7) == 7) {
 #pragma unroll
-              for (int u = jj - 7; u <= jj; ++u) CSS_PIN(acc[u]);
+              for (int u = jj - 7; u <= jj; ++u) CSS_PIN(A[u]);
             }
           }
           const uint64_t Pt = mk[2 * R], Nt = mk[2 * R + 1];
@@ -1670,7 +1673,7 @@ __global__ void __launch_bounds__(64, 2)
                * population and the A element across populations (css.c:281-326) */
               const bool cast_i = ((io < ao) == (jj < ao)) ? (io > jj) : (io < ao);
               const double prod = cast_i ? x86_int(vi) * vj : x86_int(vj) * vi;
-              acc[jj] += prod == -9.0;
+              A[jj] += prod == -9.0 ? 1.0 : 0.0;
             }
           }
 #pragma unroll
@@ -1688,7 +1691,7 @@ __global__ void __launch_bounds__(64, 2)
       int mo = m;
       CSS_OPAQUE_S(mo);
 #pragma unroll
-      for (int jj = 0; jj < MP; ++jj) A[jj] = (row && jj < mo) ? (double)acc[jj] : 0.0;
+      for (int jj = 0; jj < MP; ++jj) A[jj] = (row && jj < mo) ? A[jj] : 0.0;
 #pragma unroll
       for (int s = 0; s < T80_TS; ++s) {
         const int j = 4 * s + tq;
@@ -1699,6 +1702,11 @@ __global__ void __launch_bounds__(64, 2)
     CSS_PROF(0);
     /* ---- fill_averages (k_css_mds) */
     {
+      /* the lane indices rebuilt for this phase (css_lane_now): kept live from the kernel's
+       * start they were spilled at the Householder steps' register peak and reloaded here */
+      const int ln_ = css_lane_now();
+      const int i = ln_, tr = ln_ >> 2, tq = ln_ & 3;
+      const bool row = i < m, trow = T80_MAIN + tr < m;
       int unval = 0;
       double sum = 0;
       int mo = m;
@@ -1742,6 +1750,9 @@ __global__ void __launch_bounds__(64, 2)
     /* ---- B = -1/2 Z (D o D) Z by double centering */
     double zero_tol;
     {
+      const int ln_ = css_lane_now(); /* (as in fill_averages) */
+      const int i = ln_, tr = ln_ >> 2, tq = ln_ & 3, R = T80_MAIN + tr;
+      const bool row = i < m, trow = R < m;
       double rs = 0, rst = 0;
       int mo = m;
       CSS_OPAQUE_S(mo);
