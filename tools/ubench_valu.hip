@@ -73,6 +73,13 @@ __global__ void k(unsigned *out, unsigned seed) {
       if (OP == 53) asm volatile("v_mul_u32_u24_e32 %0, %0, %1" : "+v"(a[i]) : "v"(c));
       if (OP == 54) asm volatile("v_mul_hi_u32 %0, %0, %1" : "+v"(a[i]) : "v"(c2));
       if (OP == 55) asm volatile("v_max_i16 %0, %0, %1" : "+v"(a[i]) : "v"(c));
+      if (OP == 56) asm volatile("v_med3_u16 %0, %0, %1, %2" : "+v"(a[i]) : "v"(c), "v"(c2));
+      if (OP == 57) asm volatile("v_med3_i16 %0, %0, %1, %2" : "+v"(a[i]) : "v"(c), "v"(c2));
+      if (OP == 58) asm volatile("v_max_u16 %0, %0, %1" : "+v"(a[i]) : "v"(c));
+      if (OP == 59) asm volatile("v_min_u16 %0, %0, %1" : "+v"(a[i]) : "v"(c));
+      if (OP == 60) asm volatile("v_max_u16_sdwa %0, %0, %1 dst_sel:WORD_0 dst_unused:UNUSED_PRESERVE src0_sel:WORD_0 src1_sel:WORD_1" : "+v"(a[i]) : "v"(c));
+      if (OP == 61) asm volatile("v_max_u32_e32 %0, %0, %1" : "+v"(a[i]) : "v"(c));
+      if (OP == 62) asm volatile("v_min_i16 %0, %0, %1" : "+v"(a[i]) : "v"(c));
     }
   }
   unsigned s = 0;
@@ -153,5 +160,12 @@ int main() {
   printf("v_mul_u32_u24 e32%.1f\n", run<53>(o));
   printf("v_mul_hi_u32 x2  %.1f\n", run<54>(o));
   printf("v_max_i16        %.1f\n", run<55>(o));
+  printf("v_med3_u16       %.1f\n", run<56>(o));
+  printf("v_med3_i16       %.1f\n", run<57>(o));
+  printf("v_max_u16        %.1f\n", run<58>(o));
+  printf("v_min_u16        %.1f\n", run<59>(o));
+  printf("v_max_u16 sdwa   %.1f\n", run<60>(o));
+  printf("v_max_u32 e32 rep%.1f\n", run<61>(o));
+  printf("v_min_i16        %.1f\n", run<62>(o));
   return 0;
 }
