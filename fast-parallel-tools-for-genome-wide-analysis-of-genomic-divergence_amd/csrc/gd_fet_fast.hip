@@ -159,12 +159,49 @@ __device__ __forceinline__ uint32_t fw_key(uint32_t u, uint32_t m_lo, uint32_t m
 __device__ __forceinline__ int fw_key_index(uint32_t key, uint32_t D) {
   return (int)((((uint64_t)key + 1) * D) >> 33); /* (u mod D) >> 1 = r mod n */
 }
+__device__ __forceinline__ int64_t fw_key16_index(uint32_t key, uint32_t D) {
+  return (int64_t)((((uint64_t)key + 1) * D) >> 17); /* the same from a 16-bit key (~0: no key) */
+}
+
+/* FW_KEY16: the top list holds 16-bit keys (the low halves of its registers) and inserts with
+ * v_min_u16 / v_max_u16, 2-cycle instructions (ubench), 2 MT - 1 of them, where the u32 form
+ * issues MT 4-cycle v_med3_u32 / v_max_u32.  The key's low 16 bits suffice when M is taken as
+ * M16 = ceil(2^48 / D) = ceil(M / 2^16): then (M16 u mod 2^64) >> 32 has bits 32..47 of
+ * M16 u mod 2^48 in its low half, key16 = floor(2^16 frac(u / D + e)) with 0 <= e < 2^-16, so
+ * consecutive residues lie >= 2^16 / D - 1 >= 127 apart (D <= 512) and
+ * u mod D = ((key16 + 1) D) >> 16 (tests/test_fet_key.py pins both for every n).  Off by
+ * default: bit-exact on the FET GPU suite, but C2 2.36-2.39 against 2.34-2.35 ms/step (the
+ * seven 16-bit ops cost more than the four VOP3 ones they replace in this instruction mix). */
+#ifndef FW_KEY16
+#define FW_KEY16 0
+#endif
+__device__ __forceinline__ uint32_t min16(uint32_t a, uint32_t b) {
+  uint32_t r;
+  asm("v_min_u16 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ uint32_t max16(uint32_t a, uint32_t b) {
+  uint32_t r;
+  asm("v_max_u16 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
 
 template <int MT>
 __device__ __forceinline__ void top_insert_u(uint32_t (&K)[MT], uint32_t v) {
+#if FW_KEY16
+  /* the value displaced from slot i moves on to slot i + 1 */
+#pragma unroll
+  for (int i = 0; i < MT - 1; ++i) {
+    const uint32_t t = min16(K[i], v);
+    K[i] = max16(K[i], v);
+    v = t;
+  }
+  K[MT - 1] = max16(K[MT - 1], v);
+#else
 #pragma unroll
   for (int i = MT - 1; i > 0; --i) K[i] = max(min(K[i - 1], K[i]), min(max(K[i - 1], K[i]), v)); /* v_med3_u32 */
   K[0] = max(K[0], v);
+#endif
 }
 
 /* one draw: advance, order key, insert into the top-MT list */
@@ -227,9 +264,20 @@ __device__ __forceinline__ uint16_t pick_rix(const uint32_t (&K)[MT], int m, uin
       if (i == m - 2) kb = K[i];
     }
   }
+#if FW_KEY16
+  /* (key16 + 1) D 2^7 - base 2^24 (mod 2^32): rank - base in byte 3 (the product is below 2^33,
+   * the fraction below 2^24, so the wrap keeps the byte) */
+  ka &= 0xFFFFu;
+  kb &= 0xFFFFu;
+  wkey = min(wkey, ka);
+  const uint32_t a32 = (uint32_t)add7;
+  const uint32_t ha = __umul24(ka, D7) + a32, hb = __umul24(kb, D7) + a32;
+  return (uint16_t)__builtin_amdgcn_perm(hb, ha, 0x0C0C0703u);
+#else
   wkey = min(wkey, ka); /* a = t_{m-1} <= b = t_{m-2}: the lowest index read */
   const uint32_t ha = (uint32_t)(((uint64_t)ka * D7 + add7) >> 32), hb = (uint32_t)(((uint64_t)kb * D7 + add7) >> 32);
   return (uint16_t)__builtin_amdgcn_perm(hb, ha, 0x0C0C0501u);
+#endif
 }
 
 /* Lane q's replicates: whole replicates 12q .. 12q + 11 from y (stream position 12qn),
@@ -245,8 +293,14 @@ template <int MT, int MU>
 __device__ __forceinline__ void boot_lane(uint64_t y, uint64_t yh, int n, int nlo8, int nhi, int hlen, int hlo8,
                                           int hhi, uint64_t M, int m, int base, uint16_t *rix, uint16_t *rix_half,
                                           bool store_half, uint32_t &ymax, uint32_t &wkey) {
+#if FW_KEY16
+  const uint64_t MK = (M + 0xFFFFu) >> 16; /* ceil(2^48 / 2n) */
+  const uint32_t mlo = (uint32_t)MK, mhi = (uint32_t)(MK >> 32), D7 = 256u * (uint32_t)n;
+  const uint64_t add7 = (uint32_t)(D7 - ((uint32_t)base << 24));
+#else
   const uint32_t mlo = (uint32_t)M, mhi = (uint32_t)(M >> 32), D7 = 256u * (uint32_t)n;
   const uint64_t add7 = (uint64_t)D7 - ((uint64_t)base << 40);
+#endif
   uint32_t ylo = (uint32_t)y, yhi = (uint32_t)(y >> 32);
 #pragma unroll 2
   for (int k = 0; k < FW_RPT; ++k) {
@@ -810,7 +864,11 @@ __global__ void __launch_bounds__(FW_WPB *FW_TPW) FW_WPE
       FW_BOOT(8, 0);
     }
 #undef FW_BOOT
+#if FW_KEY16
+    if (fw_key16_index(wkey, 2u * (uint32_t)n) < base) atomicOr(&sh_bad[wl], FW_BAD_GENERAL);
+#else
     if (fw_key_index(wkey, 2u * (uint32_t)n) < base) atomicOr(&sh_bad[wl], FW_BAD_GENERAL);
+#endif
     if ((ymax >> 1) > limit) atomicOr(&sh_bad[wl], FW_BAD_REJECT);
   }
 #else

@@ -55,3 +55,36 @@ def test_key_matches_remainder_draws():
             r = x >> 17
             key = ((M * u) & MASK64) >> 32
             assert ((key + 1) * D) >> 33 == r % n
+
+
+def key16_np(u, n):
+    """FW_KEY16: the low half of (M16 u mod 2^64) >> 32, M16 = ceil(M / 2^16) = ceil(2^48 / 2n)."""
+    D = 2 * n
+    M16 = np.uint64(((MASK64 // D + 1) + 0xFFFF) >> 16)
+    return ((u * M16) >> np.uint64(32)) & np.uint64(0xFFFF)
+
+
+def test_key16_recovers_residue_and_orders():
+    rng = np.random.default_rng(12)
+    base = rng.integers(0, 1 << 32, 40000, dtype=np.uint64)
+    for n in range(1, 257):
+        D = 2 * n
+        top = np.uint64((1 << 32) - 1)
+        edges = np.array([0, 1, D - 1, D, D + 1], dtype=np.uint64)
+        hi = top - np.arange(0, 3 * D, dtype=np.uint64)
+        u = np.concatenate([base, edges, hi])
+        k = key16_np(u, n)
+        res = u % np.uint64(D)
+        idx = ((k + np.uint64(1)) * np.uint64(D)) >> np.uint64(17)
+        assert np.array_equal(idx, res >> np.uint64(1)), n
+        kmax = np.zeros(D, dtype=np.int64) - 1
+        kmin = np.full(D, 1 << 40, dtype=np.int64)
+        np.maximum.at(kmax, res.astype(np.int64), k.astype(np.int64))
+        np.minimum.at(kmin, res.astype(np.int64), k.astype(np.int64))
+        seen = kmax >= 0
+        assert np.all(kmax[seen][:-1] < kmin[seen][1:]), n
+        # pick_rix's packed form: ((key16 + 1) 256 n - base 2^24) mod 2^32, byte 3 = index - base
+        for b in (0, 1, min(7, n - 1), n - 1):
+            sel = (idx >= np.uint64(b))
+            t = ((k[sel] * np.uint64(256 * n) + np.uint64((256 * n - (b << 24)) & 0xFFFFFFFF)) & np.uint64(0xFFFFFFFF))
+            assert np.array_equal(t >> np.uint64(24), (idx[sel] - np.uint64(b)) & np.uint64(0xFF)), (n, b)
