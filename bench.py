@@ -85,6 +85,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target wall time of each CSS CPU sample")
     ap.add_argument("--backend", default="nccl")
     ap.add_argument("--dry-run", action="store_true", help="distributed plumbing only, no GPU work (CPU tests)")
+    ap.add_argument("--trace-hang", type=float, default=0.0,
+                    help="dump every thread's Python stack to stderr every SECONDS (diagnostics)")
     ap.add_argument("--force-dist", action="store_true",
                     help="initialise torch.distributed even at one rank (exercises the RCCL gathers on one GPU)")
     return ap.parse_args()
@@ -639,6 +641,12 @@ def c45_leg(env, args, name, treshold, runs, queue):
            "sharding": "store-counter ticket queue, input generated per pulled ticket (2 slots)" if queue
            else "plan_shards (LPT by SNP count), whole chromosomes per rank",
            "resident_input_bytes_per_rank": int(nbuf * alen * 24)}
+    perm_ms = float(stage[1])
+    if env.dist and runs > 0:  # GPU-time of the permutation kernel summed over ranks (every rank
+        # takes part, before the ranks other than 0 return below)
+        t = torch.tensor([perm_ms], dtype=torch.float64, device=env.cdev)
+        env.dist.all_reduce(t)
+        perm_ms = float(t.item())
     # the one collective: (score, p) of every rank's chromosomes, gathered to rank 0
     if env.dist:
         shard_done = gather_lists(mine) if queue else shards
@@ -672,11 +680,6 @@ def c45_leg(env, args, name, treshold, runs, queue):
             out["distance_build"] = db
     out["mean_p"] = float(pm[computed].mean()) if computed.any() else None
     if runs > 0 and computed.any():
-        perm_ms = float(stage[1])
-        if env.dist:  # GPU-time of the permutation kernel summed over ranks
-            t = torch.tensor([perm_ms], dtype=torch.float64, device=env.cdev)
-            env.dist.all_reduce(t)
-            perm_ms = float(t.item())
         out["permutations"] = perm_stats(pm, computed, treshold, runs, perm_ms, pop)
         pv_ = css_valu("c5_perm", mine_w, float(stage[1]))
         out["permutations"].update(pv_)
@@ -743,8 +746,17 @@ def dry_run(args, rank, world, dist):
 
 
 # ----------------------------------------------------------------------------- main
+def note(rank, msg):
+    """a progress line on stderr (rank 0): the JSON line on stdout stays the only output there"""
+    if rank == 0:
+        print(f"bench: {msg} ({time.strftime('%H:%M:%S')})", file=sys.stderr, flush=True)
+
+
 def main():
     args = parse()
+    if args.trace_hang > 0:
+        import faulthandler
+        faulthandler.dump_traceback_later(args.trace_hang, repeat=True, file=sys.stderr)
     rc = maybe_launch(args)
     if rc is not None:
         sys.exit(rc)
@@ -828,6 +840,7 @@ def main():
                                      bpos.data_ptr(), args.wsize, args.wstep, args.perc,
                                      _lib.GD_WINDOWS_THREADED, scores.data_ptr(), stddev.data_ptr(), stream))
 
+    note(rank, f"FET: {world} rank(s), {windows} windows per rank")
     for _ in range(args.warmup):
         step()
     stage = np.zeros(_lib.GD_NSTAGES)
@@ -916,6 +929,7 @@ def main():
         },
         "roofline": roof,
     }
+    note(rank, f"FET: {ms_per_step:.3f} ms/step")
     if rank == 0 and world == 1 and not args.no_cpu:
         cb = fet_cpu_baseline(args, scores, chroms)
         sources["cpu_baseline"] = cb.pop("what")
@@ -924,6 +938,7 @@ def main():
                        "general_path": float(stage[2]), "scan_total": float(stage[3])}
 
     if not args.no_extra:
+        note(rank, "region-filter and packed-track legs")
         out["regions"] = regions_run(args, scores, stddev, chroms, nch, rank, world, dev)
         out["packed"], codes = packed_run(args, lib, _lib, check, ctx, stream, dev, avals, bvals, apos, bpos, chroms,
                                           nch, scores, stddev)
@@ -933,12 +948,15 @@ def main():
         del codes
 
     if not args.no_css:
+        note(rank, "CSS C3")
         css = {"c3": c3_leg(env, args, chroms, nch, windows, avals, bvals, apos, bpos, scores)}
         del avals, bvals, apos, bpos, scores, stddev
         torch.cuda.empty_cache()
         if not args.no_c45:
+            note(rank, "CSS C4")
             css["c4"] = c45_leg(env, args, "c4", 10, 0, queue=False)
             torch.cuda.empty_cache()
+            note(rank, "CSS C5")
             css["c5"] = c45_leg(env, args, "c5", 10, 1000, queue=True)
         out["css"] = css
         if CSS_VALU_FILE.exists():

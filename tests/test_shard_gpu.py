@@ -105,3 +105,36 @@ def test_rccl_device_tensor_gathers_one_rank():
     assert out["config"]["collective_backend"] == "nccl" and out["config"]["track_gather_ms"] is not None
     assert out["css"]["c4"]["track_gather_ms"] is not None and out["css"]["c5"]["track_gather_ms"] is not None
     assert out["css"]["c5"]["resident_input_bytes_per_rank"] == 2 * 60000 * 40 * 24
+
+
+def test_bench_two_ranks_one_gpu():
+    """bench.py at --gpus 2 as the driver launches it (torch.distributed.run, two ranks),
+    both ranks on cuda:0 over gloo: every leg's collectives are entered by every rank in the
+    same order (a rank-0-only all-reduce after the other ranks had returned once hung the C5
+    leg), the C5 queue hands every chromosome to exactly one rank, and rank 0 prints the line."""
+    import json
+    import signal
+    import subprocess
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parent.parent
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), str(root / "bench.py"), "--gpus", "2",
+           "--steps", "2", "--warmup", "1", "--nchrom", "1", "--nsnp", "60000", "--no-extra", "--css-steps", "1",
+           "--c45-chroms", "2", "--c45-steps", "1"]
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env, cwd=root,
+                         start_new_session=True)
+    try:
+        so, se = p.communicate(timeout=240)
+    except subprocess.TimeoutExpired:
+        os.killpg(p.pid, signal.SIGKILL)
+        p.communicate()
+        raise AssertionError("two-rank bench did not finish in 240 s")
+    assert p.returncode == 0, se[-3000:]
+    out = json.loads(so.strip().splitlines()[-1])
+    assert out["n_gpus"] == 2 and out["config"]["collective_backend"] == "gloo"
+    assert out["config"]["track_gather_ms"] is not None
+    c5 = out["css"]["c5"]
+    assert sum(c5["chromosomes_per_rank"]) == 4 and c5["track_gather_ms"] is not None
+    assert c5["permutations"]["total"] > 0
