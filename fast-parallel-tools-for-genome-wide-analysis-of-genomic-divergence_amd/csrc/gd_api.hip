@@ -524,12 +524,18 @@ static int fet_scan_locked(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, cons
     HIP_TRY(hipEventRecord(ctx->gev[g], sm));
   }
   HIP_TRY(hipEventRecord(ctx->ev[1], sm));
+  /* GD_WALT=1 (with G > 1): the groups' window kernels alternate between stream2 and the
+   * caller's stream, so two of them can run at once (their outputs and the declined-window
+   * list are disjoint / atomic) */
+  const char *walt = getenv("GD_WALT");
+  const bool alt = G > 1 && walt && walt[0] == '1';
   for (int g = 0; g < G && !force_general; ++g) {
     const int c0 = cuts[g], c1 = cuts[g + 1];
-    if (G > 1) HIP_TRY(hipStreamWaitEvent(s2, ctx->gev[g], 0));
+    hipStream_t sw = (alt && (g & 1)) ? s : s2;
+    if (G > 1) HIP_TRY(hipStreamWaitEvent(sw, ctx->gev[g], 0));
     st = gd_fet_window_fast_launch(d_ch, nchrom, d_blk, blk_off[c0], blk_off[c1] - blk_off[c0], lo_a, hi_a, lo_b,
                                    snp, avals, bvals, binom, ctx->lut_hdr, ctx->lut, fused ? 1 : 0, perc, scores,
-                                   stddev, flags, list, list_count, s2);
+                                   stddev, flags, list, list_count, sw);
     if (st) return fail(st, "fast window kernel launch failed");
   }
   HIP_TRY(hipEventRecord(ctx->ev[2], s2));
