@@ -524,11 +524,11 @@ static int fet_scan_locked(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, cons
     HIP_TRY(hipEventRecord(ctx->gev[g], sm));
   }
   HIP_TRY(hipEventRecord(ctx->ev[1], sm));
-  /* GD_WALT=1 (with G > 1): the groups' window kernels alternate between stream2 and the
-   * caller's stream, so two of them can run at once (their outputs and the declined-window
-   * list are disjoint / atomic) */
+  /* with G > 1 the groups' window kernels alternate between stream2 and the caller's stream,
+   * so two of them run at once (their outputs are disjoint, the declined-window list and the
+   * flags atomic); GD_WALT=0 keeps them all on stream2 (diagnostics) */
   const char *walt = getenv("GD_WALT");
-  const bool alt = G > 1 && walt && walt[0] == '1';
+  const bool alt = G > 1 && !(walt && walt[0] == '0');
   for (int g = 0; g < G && !force_general; ++g) {
     const int c0 = cuts[g], c1 = cuts[g + 1];
     hipStream_t sw = (alt && (g & 1)) ? s : s2;

@@ -34,7 +34,9 @@ typedef struct gd_chrom_dev {
 /* general-path window capacity held in LDS; larger windows use global scratch */
 #define GD_GEN_LDS_N 1024
 #define GD_MAX_GROUPS 32    /* chromosome groups pipelined across two streams (capacity) */
-#define GD_DEFAULT_GROUPS 1 /* groups used by default (r03 sweeps: with the coalesced k_bounds 1 group 2.58, 2 groups 2.64 ms per C2 scan) */
+#define GD_DEFAULT_GROUPS 2 /* groups used by default, their window kernels on alternating streams (r04: 2.288-2.317
+                               against 2.312-2.339 ms per C2 scan with one group; r03, without the alternation, 2 groups
+                               were slower: 2.64 against 2.58) */
 #define GD_LUT_CAP (1 << 22) /* FET score-table entries (32 MB): up to ~62+62 individuals */
 #define GD_NREP 100 /* bootstrap replicates (cFisher.c:62) */
 

@@ -160,13 +160,16 @@ def test_device_synth_matches_numpy():
         assert np.array_equal(x.cpu().numpy(), y)
 
 
-@pytest.mark.parametrize("groups", [None, "2", "4"])
+@pytest.mark.parametrize("groups", [None, "1", "2", "4", "2s", "4s"])
 def test_device_batch_api_matches_host(oracle, monkeypatch, groups):
     """Several chromosomes in one device scan == per-chromosome scans; with GD_GROUPS the
-    scan pipelines chromosome groups over the context's two streams (the default, one
-    group, runs every pass on the caller's stream)."""
+    scan pipelines chromosome groups over the context's streams (the default, two groups,
+    their window kernels on alternating streams, running concurrently; one group runs every
+    pass on the caller's stream); "s": GD_WALT=0, every window kernel on one stream."""
     if groups:
-        monkeypatch.setenv("GD_GROUPS", groups)
+        monkeypatch.setenv("GD_GROUPS", groups.rstrip("s"))
+        if groups.endswith("s"):
+            monkeypatch.setenv("GD_WALT", "0")
     import torch
     from gdscan import _lib, synth
     from gdscan._lib import Chrom, check, lib
