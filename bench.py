@@ -411,10 +411,12 @@ class Env:
         from gdscan import _lib, synth
         from gdscan._lib import Chrom, check, lib
         self.args, self.rank, self.world, self.dist = args, rank, world, dist
+        if args.dry_run:
+            lib = DryLib(lib)
         self.torch, self._lib, self.synth, self.Chrom, self.check, self.lib = torch, _lib, synth, Chrom, check, lib
-        self.dev = torch.device("cuda", local)
+        self.dev = torch.device("cpu") if args.dry_run else torch.device("cuda", local)
         # gloo (ranks sharing a GPU, or --backend gloo) reduces host tensors; RCCL device ones
-        self.cdev = torch.device("cpu") if dist and dist.get_backend() == "gloo" else self.dev
+        self.cdev = torch.device("cpu") if (dist and dist.get_backend() == "gloo") or args.dry_run else self.dev
         self.stream = torch.cuda.current_stream(self.dev).cuda_stream
         self.ctx = lib.gd_ctx_create(local)
         assert self.ctx, "gd_ctx_create failed"
@@ -518,12 +520,13 @@ def c3_leg(env, args, chroms, nch, windows, avals, bvals, apos, bpos, scores):
            "ms_mean": float(np.mean(ts)) * 1e3, "steps": args.css_steps,
            "workload": f"configs[2] shape: {nch} x {args.nsnp} SNPs per GPU, {args.asize}+{args.bsize}, runs=0",
            "windows_per_gpu": windows, "kernel_ms": kmed,
-           "fp64_frac": flops / (kmed * 1e-3) / 1e12 / FP64_PEAK_TFLOPS, "alg_flops_per_window": flops / windows}
+           "fp64_frac": flops / (kmed * 1e-3) / 1e12 / FP64_PEAK_TFLOPS if kmed > 0 else 0.0,
+           "alg_flops_per_window": flops / max(windows, 1)}
     out.update(css_valu("c3", windows, kmed))
     db = dist_build("c3", m, kmed, windows)
     if db:
         out["distance_build"] = db
-    if env.rank == 0 and env.world == 1 and not args.no_cpu:
+    if env.rank == 0 and not args.no_cpu and not args.dry_run:
         out["cpu_baseline"] = css_cpu_baseline(args, args.asize, 10, 0)
     return out
 
@@ -662,6 +665,8 @@ def c45_leg(env, args, name, treshold, runs, queue):
         out["track_gather_ms"] = env.max_over_ranks((time.perf_counter() - g0) * 1e3)
         if queue:
             out["chromosomes_per_rank"] = [len(x) for x in shard_done]
+            # the queue hands every chromosome to exactly one rank
+            out["queue_each_once"] = sorted(c for x in shard_done for c in x) == list(range(total))
         if rank != 0:
             return out
         sc_all, p_all = track[:, 0], track[:, 1]
@@ -688,13 +693,58 @@ def c45_leg(env, args, name, treshold, runs, queue):
             mf = doc["mfma"]
             busy = mf["busy_simd_cycles_per_dispatch"] / doc["windows_per_dispatch"] * mine_w
             out["permutations"]["mfma_busy"] = busy / (1024 * 2.4e9 * stage[1] * 1e-3)
-    if env.rank == 0 and env.world == 1 and not args.no_cpu:
+    if env.rank == 0 and not args.no_cpu and not args.dry_run:
         out["cpu_baseline"] = css_cpu_baseline(args, pop, treshold, runs)
     del av, bv, ap, bp
     return out
 
 
 # ----------------------------------------------------------------------------- dry run (CPU)
+class _DryStream:
+    cuda_stream = 0
+
+    def wait_event(self, _e):
+        pass
+
+    def synchronize(self):
+        pass
+
+
+class _DryEvent:
+    def record(self, _stream=None):
+        pass
+
+    def synchronize(self):
+        pass
+
+
+def install_dry_cuda(torch):
+    """--dry-run: the torch.cuda calls the legs make become no-ops on the CPU"""
+    c = torch.cuda
+    c.synchronize = lambda *a, **k: None
+    c.current_stream = lambda *a, **k: _DryStream()
+    c.Stream = lambda *a, **k: _DryStream()
+    c.Event = lambda *a, **k: _DryEvent()
+    c.empty_cache = lambda: None
+    c.set_device = lambda *a, **k: None
+
+
+class DryLib:
+    """--dry-run: libgdscan with its device entry points as no-ops (status GD_OK); every other
+    symbol (window counts, modes, stage times) is the real library's host code"""
+    DEVICE = {"gd_ctx_create": 1, "gd_ctx_destroy": None, "gd_synth_device": 0, "gd_fet_scan_device": 0,
+              "gd_css_scan_device": 0, "gd_pack_chrom_device": 0, "gd_fet_scan_packed_device": 0}
+
+    def __init__(self, real):
+        self._real = real
+
+    def __getattr__(self, name):
+        if name in DryLib.DEVICE:
+            v = DryLib.DEVICE[name]
+            return lambda *a: v
+        return getattr(self._real, name)
+
+
 def dry_run(args, rank, world, dist):
     """The distributed plumbing without a GPU: shard plan, the chromosome queue over the
     default store with the input moving with the ticket (queue_pull_pipelined: a rank
@@ -736,13 +786,12 @@ def dry_run(args, rank, world, dist):
     ok0 = gather_lists([int(ok0)])
     made_all = gather_lists(made)
     shards = plan_shards([args.nsnp] * total, world)
-    if rank == 0:
-        print(json.dumps({"dry_run": True, "n_gpus": world, "backend": args.backend, "queue_per_rank":
-                          [len(s) for s in lists], "static_per_rank": [len(s) for s in shards], "gather_ok": ok,
-                          "gather_to_0_ok": all(x[0] == 1 for x in ok0),
-                          "materialised_only_pulled": all(sorted(m) == sorted(d) for m, d in zip(made_all, lists)),
-                          "max_live_inputs": peak[0]}), flush=True)
     dist.barrier()
+    return {"dry_run": True, "n_gpus": world, "backend": args.backend, "queue_per_rank":
+            [len(s) for s in lists], "static_per_rank": [len(s) for s in shards], "gather_ok": ok,
+            "gather_to_0_ok": all(x[0] == 1 for x in ok0),
+            "materialised_only_pulled": all(sorted(m) == sorted(d) for m, d in zip(made_all, lists)),
+            "max_live_inputs": peak[0]}
 
 
 # ----------------------------------------------------------------------------- main
@@ -766,24 +815,30 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))
     dist = None
+    plumbing = None
     if args.dry_run:
-        import torch.distributed as dist_mod
-        if world > 1:
-            dist_mod.init_process_group(args.backend)
-            dry_run(args, rank, world, dist_mod)
-            dist_mod.destroy_process_group()
-        else:
+        # the distributed plumbing checks, then every leg in the bench's real order with the
+        # device work stubbed out (install_dry_cuda, DryLib): the same collectives, barriers
+        # and queue pulls as a GPU run, on CPU tensors over gloo
+        if world == 1:
             print(json.dumps({"dry_run": True, "n_gpus": 1}), flush=True)
-        return
+            return
+        import torch.distributed as dist_mod
+        args.backend = "gloo"
+        args.no_extra = args.no_cpu = True  # host-buffer and CPU-baseline legs need the device results
+        dist_mod.init_process_group("gloo")
+        dist = dist_mod
+        plumbing = dry_run(args, rank, world, dist_mod)
+        install_dry_cuda(torch)
     # more ranks than GPUs (a rehearsal of --gpus N on a smaller box): ranks share the
     # devices round-robin, and the collectives go over gloo (RCCL refuses two ranks on one
     # GPU); device_count() does not initialise the GPU
     from gdscan.shard import choose_backend
-    ndev = max(1, torch.cuda.device_count())
+    ndev = 1 if args.dry_run else max(1, torch.cuda.device_count())
     args.backend, _on_device = choose_backend(world, ndev, args.backend)
     local = local % ndev
     torch.cuda.set_device(local)
-    if world > 1 or args.force_dist:
+    if (world > 1 or args.force_dist) and dist is None:
         import torch.distributed as dist_mod
         if world == 1:  # --force-dist: a one-rank group, so the collectives really run (RCCL on the GPU)
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -818,6 +873,8 @@ def main():
     torch.cuda.synchronize()
     # regend of each chromosome = last position + 1
     last = apos.view(nch, alen)[:, -1].cpu().numpy().astype(np.int64)
+    if args.dry_run:  # no generator ran: the host restatement of its positions
+        last = np.array([synth.regend(rank * nch + c, nsnp) - 1 for c in range(nch)], dtype=np.int64)
     chroms = (env.Chrom * nch)()
     w_out = 0
     windows = 0
@@ -873,7 +930,7 @@ def main():
 
     kernel_ms = float(stage[_lib.GD_NSTAGES - 1])  # first kernel -> last kernel of the scan
     alg_bytes = 12.0 * (nch * (alen + blen)) + 16.0 * windows
-    achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
+    achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9 if kernel_ms > 0 else 0.0
     sources = {}
     roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, "traffic": None, "alg_bytes_per_step": alg_bytes,
@@ -889,7 +946,7 @@ def main():
         # scan time against one wave64 instruction per SIMD per 4 cycles, and the window
         # kernel's own VALU busy fraction from its SQ counters
         vr = json.loads(VALU_FILE.read_text())
-        if vr.get("config") == [nch, nsnp, a, b]:
+        if vr.get("config") == [nch, nsnp, a, b] and kernel_ms > 0:
             roof["valu_ginsts"] = vr["valu_wave_insts_per_scan"] / (kernel_ms * 1e-3) / 1e9
             roof["valu_issue_peak_ginsts"] = VALU_ISSUE_GINSTS
             roof["valu_frac"] = roof["valu_ginsts"] / VALU_ISSUE_GINSTS
@@ -930,12 +987,14 @@ def main():
         "roofline": roof,
     }
     note(rank, f"FET: {ms_per_step:.3f} ms/step")
-    if rank == 0 and world == 1 and not args.no_cpu:
+    if rank == 0 and not args.no_cpu and not args.dry_run:
+        # after the timed region, at any world size: the other ranks wait at the next leg's barrier
         cb = fet_cpu_baseline(args, scores, chroms)
         sources["cpu_baseline"] = cb.pop("what")
         out["cpu_baseline"] = cb
-    out["stage_ms"] = {"hbm_passes_done": float(stage[0]), "fast_windows_done": float(stage[1]),
-                       "general_path": float(stage[2]), "scan_total": float(stage[3])}
+    # HIP events of the last scans, from the scan's first kernel (include/gdscan.h GD_STAGE_*)
+    out["stage_ms"] = {"prologue": float(stage[0]), "through_window_kernels": float(stage[1]),
+                       "general_path": float(stage[2]), "scan": float(stage[3])}
 
     if not args.no_extra:
         note(rank, "region-filter and packed-track legs")
@@ -968,10 +1027,14 @@ def main():
         sources["css_cpu"] = "oracle/css_oracle.c threaded over the host cores (the reference CSS needs GSL, absent)"
     lib.gd_ctx_destroy(ctx)
     out["sources"] = sources
+    if plumbing is not None:
+        out.update(plumbing)
     if rank == 0:
         print(json.dumps(out, separators=(",", ":")), flush=True)
     if dist:
         dist.barrier()
+        if args.dry_run:
+            print(f"bench: rank {rank} reached the final barrier", file=sys.stderr, flush=True)
         dist.destroy_process_group()
 
 

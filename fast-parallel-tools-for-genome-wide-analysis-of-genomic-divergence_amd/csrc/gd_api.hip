@@ -53,6 +53,14 @@ int gd_pack_device_launch(const double *avals, const double *bvals, const int32_
                           int asize, int bsize, int nrows, uint64_t *acodes, uint64_t *bcodes, int32_t *rowpos,
                           unsigned *bad, hipStream_t s);
 int gd_fet_fast_windows_per_block();
+__global__ void k_fet_setup(gd_chrom_dev *ch, int nchrom, const int32_t *apos, const int32_t *bpos, unsigned *flags,
+                            const uint64_t *binom, int *hdr, double *lut, int64_t cap, unsigned *done);
+int gd_fet_window_sched_launch(const gd_chrom_dev *ch, int nchrom, const int32_t *blk_off, int blk_count,
+                               int32_t *lo_a, int32_t *hi_a, int32_t *lo_b, const double *snp_score,
+                               const double *avals, const double *bvals, const uint64_t *binom, const int *lut_hdr,
+                               const double *lut, double perc, double *scores, double *stddev, unsigned *flags,
+                               int32_t *slow_list, unsigned *slow_count, const gd_fet_sched *d_sc, int nb,
+                               hipStream_t s);
 int gd_bounds_elems_per_block();
 int gd_fet_fast_init(hipStream_t s);
 int gd_fet_window_prepare(int64_t wtotal, int32_t *slow_list, unsigned *slow_count, hipStream_t s,
@@ -139,6 +147,8 @@ struct gd_ctx {
   unsigned *h_flags = nullptr; /* pinned */
   char *h_stage = nullptr;     /* pinned staging of the per-call descriptors (h2d) */
   size_t h_stage_cap = 0, h_stage_off = 0;
+  hipEvent_t stage_ev = nullptr; /* after the last copy out of h_stage (recorded by h2d) */
+  bool stage_live = false;       /* stage_ev was recorded since the buffer was last reset */
   unsigned *h_flags_dev = nullptr; /* one device word (packer status) */
 };
 
@@ -178,6 +188,7 @@ static int ctx_init(gd_ctx *c, int device) {
                       hipMemcpyHostToDevice));
   }
   for (auto &e : c->ev) HIP_TRY(hipEventCreate(&e));
+  HIP_TRY(hipEventCreateWithFlags(&c->stage_ev, hipEventDisableTiming));
   HIP_TRY(hipMalloc(&c->lut_hdr, 4 * sizeof(int)));
   HIP_TRY(hipMemsetAsync(c->lut_hdr, 0, 4 * sizeof(int), c->stream));
   HIP_TRY(hipMalloc(&c->lut, sizeof(double) * GD_LUT_CAP));
@@ -211,6 +222,10 @@ extern "C" void gd_ctx_destroy(gd_ctx *c) {
     if (e) (void)hipEventDestroy(e);
   for (auto &e : c->gev)
     if (e) (void)hipEventDestroy(e);
+  if (c->stage_ev) {
+    (void)hipEventSynchronize(c->stage_ev);
+    (void)hipEventDestroy(c->stage_ev);
+  }
   if (c->stream2) (void)hipStreamDestroy(c->stream2);
   if (c->stream_mem) (void)hipStreamDestroy(c->stream_mem);
   if (c->h_flags) (void)hipHostFree(c->h_flags);
@@ -378,12 +393,23 @@ static int make_plan_packed(const PackedIn &pk, int nchrom, int wsize, int wstep
 
 /* Host -> device copy of a per-call descriptor array through the context's pinned
  * staging buffer, so the copy is a plain asynchronous DMA (a pageable source makes
- * hipMemcpyAsync stage it synchronously).  Every scan call ends with a stream sync, so
- * the buffer is free again at the next call (h_stage_off is reset there). */
+ * hipMemcpyAsync stage it synchronously).  stage_ev follows the last staged copy: a call
+ * starts by waiting for it (stage_reset) before it rewrites the buffer, so a call that
+ * returned early on an error path, before its stream sync, cannot leave a DMA reading
+ * memory the next call overwrites. */
+static int stage_reset(gd_ctx *c) {
+  if (c->stage_live) HIP_TRY(hipEventSynchronize(c->stage_ev));
+  c->stage_live = false;
+  c->h_stage_off = 0;
+  return GD_OK;
+}
+
 static int h2d(gd_ctx *c, void *dst, const void *src, size_t bytes, hipStream_t s) {
   const size_t need = (c->h_stage_off + bytes + 255) & ~(size_t)255;
   if (need > c->h_stage_cap) {
-    HIP_TRY(hipStreamSynchronize(s)); /* earlier staged copies of this call have landed */
+    /* every staged copy so far (this call's, on s) has landed before the buffer is freed */
+    if (c->stage_live) HIP_TRY(hipEventSynchronize(c->stage_ev));
+    c->stage_live = false;
     if (c->h_stage) (void)hipHostFree(c->h_stage);
     c->h_stage = nullptr;
     c->h_stage_cap = 0;
@@ -396,6 +422,8 @@ static int h2d(gd_ctx *c, void *dst, const void *src, size_t bytes, hipStream_t 
   std::memcpy(p, src, bytes);
   c->h_stage_off = (c->h_stage_off + bytes + 255) & ~(size_t)255;
   HIP_TRY(hipMemcpyAsync(dst, p, bytes, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipEventRecord(c->stage_ev, s));
+  c->stage_live = true;
   return GD_OK;
 }
 
@@ -432,11 +460,17 @@ static int fet_scan_locked(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, cons
   for (int c = 0; c < nchrom; ++c) blk_off[c + 1] = blk_off[c] + (pl.h[c].wend + wpb - 1) / wpb;
 
   Carve cv{nullptr};
+  /* flags: [0] status bits, [4] declined-window count, [8] dense-window count, [12] the
+   * setup kernel's done counter, [13] the window kernel's ticket, [32 + bstride c]
+   * chromosome c's bounds tiles written (scheduled scan) -- all zeroed by one memset */
+  int bstride = 32; /* one 128-byte line per chromosome's counter */
+  if (const char *e = getenv("GD_FET_BSTRIDE")) bstride = std::max(1, atoi(e)); /* diagnostics */
+  const size_t nflags = 32 + (size_t)nchrom * bstride;
   auto layout = [&](Carve &k, gd_chrom_dev **d_ch, int32_t **d_blk, unsigned **flags, int32_t **lo_a,
                     int32_t **hi_a, int32_t **lo_b, double **snp, int32_t **list, int32_t **huge) {
     *d_ch = k.take<gd_chrom_dev>(nchrom);
-    *d_blk = k.take<int32_t>(nchrom + 1);
-    *flags = k.take<unsigned>(16);
+    *d_blk = k.take<int32_t>(2 * (size_t)nchrom + 2); /* workgroup offsets, then bounds-tile offsets */
+    *flags = k.take<unsigned>(nflags);
     *lo_a = k.take<int32_t>(pl.wtotal);
     *hi_a = k.take<int32_t>(pl.wtotal);
     *lo_b = k.take<int32_t>(pl.wtotal);
@@ -444,6 +478,7 @@ static int fet_scan_locked(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, cons
     *list = k.take<int32_t>(pl.wtotal);
     *huge = k.take<int32_t>(pl.wtotal);
   };
+  gd_fet_sched *d_sc = nullptr;
   gd_chrom_dev *d_ch;
   unsigned *flags;
   int32_t *d_blk, *lo_a, *hi_a, *lo_b, *list, *huge;
@@ -451,6 +486,7 @@ static int fet_scan_locked(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, cons
   int64_t *d_roff = nullptr, *d_woff = nullptr;
   auto layout_all = [&](Carve &k) {
     layout(k, &d_ch, &d_blk, &flags, &lo_a, &hi_a, &lo_b, &snp, &list, &huge);
+    d_sc = k.take<gd_fet_sched>(1);
     if (pk) {
       d_roff = k.take<int64_t>(nchrom);
       d_woff = k.take<int64_t>(2 * (size_t)nchrom);
@@ -461,87 +497,148 @@ static int fet_scan_locked(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, cons
   Carve real{ctx->ws};
   layout_all(real);
   unsigned *list_count = flags + 4, *huge_count = flags + 8;
-  ctx->h_stage_off = 0;
+  if ((st = stage_reset(ctx))) return st;
   if (pk) {
     if ((st = h2d(ctx, d_roff, row_off.data(), sizeof(int64_t) * nchrom, s))) return st;
     if ((st = h2d(ctx, d_woff, word_off.data(), sizeof(int64_t) * 2 * nchrom, s))) return st;
   }
   if ((st = h2d(ctx, d_ch, pl.h.data(), sizeof(gd_chrom_dev) * nchrom, s))) return st;
-  if ((st = h2d(ctx, d_blk, blk_off.data(), sizeof(int32_t) * (nchrom + 1), s))) return st;
-  HIP_TRY(hipMemsetAsync(flags, 0, 16 * sizeof(unsigned), s));
-  HIP_TRY(hipEventRecord(ctx->ev[0], s));
-  /* Pipeline over chromosome groups on the context's two streams: the HBM-bound
-   * passes (bounds + per-SNP FET) run on the high-priority stream and feed the
-   * VALU-bound bootstrap of each group on the low-priority stream as soon as the
-   * group's rows are scored.  The caller's stream `s` orders the scan against its
-   * other work. */
-  int G = std::min(nchrom, GD_DEFAULT_GROUPS);
-  if (const char *eg = getenv("GD_GROUPS")) G = std::max(1, std::min(std::min(nchrom, GD_MAX_GROUPS), atoi(eg))); /* diagnostics */
-  /* one group (the default): every kernel on the caller's stream, no cross-stream event waits
-   * between the passes */
-  hipStream_t sm = G > 1 ? ctx->stream_mem : s, s2 = G > 1 ? ctx->stream2 : s;
-  if (G > 1) HIP_TRY(hipStreamWaitEvent(sm, ctx->ev[0], 0));
-  if (!pk) hipLaunchKernelGGL(k_popsize, dim3(nchrom), dim3(64), 0, sm, d_ch, apos, bpos, flags);
-  bool force_general = false;
-  if ((st = gd_fet_window_prepare(pl.wtotal, list, list_count, sm, &force_general))) return st;
-  /* score table for chromosome 0's population sizes (no-op when cached) */
-  hipLaunchKernelGGL(k_fet_lut_build, dim3(512), dim3(256), 0, sm, d_ch, binom, ctx->lut_hdr, ctx->lut,
-                     (int64_t)GD_LUT_CAP);
-  hipLaunchKernelGGL(k_fet_lut_publish, dim3(1), dim3(1), 0, sm, d_ch, binom, ctx->lut_hdr, (int64_t)GD_LUT_CAP);
-
-  /* fused (default): wherever the score table holds a chromosome's sizes, the window
-   * kernel scores its own span rows from the genotype values and the per-SNP pass
-   * (k_snp_fet) exits at once, so the only full pass is k_bounds; GD_FET_UNFUSED=1
-   * restores the per-SNP pass feeding the window kernel through snp_score */
+  /* Scheduled scan (the default for reference-layout tracks): one stream, three launches --
+   * k_fet_setup (sizes, score table), the per-SNP pass (exits at once wherever the table
+   * holds the sizes), and the window kernel, whose first workgroups run the bounds pass
+   * chromosome by chromosome while the others bootstrap the windows whose bounds are done
+   * (gd_fet_fast.hip).  Opt-in while it is tuned (GD_FET_SCHED=1); the grouped two-stream
+   * pipeline below is the default. */
   const char *uf = getenv("GD_FET_UNFUSED");
   const bool fused = !pk && !(uf && uf[0] == '1'); /* packed: the per-SNP pass reads 2 bits per genotype */
-  std::vector<int> cuts(G + 1);
-  for (int g = 0; g <= G; ++g) cuts[g] = (int)((int64_t)nchrom * g / G);
-  for (int g = 0; g < G; ++g) {
-    const int c0 = cuts[g], nc = cuts[g + 1] - cuts[g];
-    if (nc <= 0) continue;
-    int64_t amax = 1, mx = 1;
-    for (int c = c0; c < c0 + nc; ++c) {
-      amax = std::max<int64_t>(amax, pl.h[c].alen);
-      mx = std::max<int64_t>(mx, std::max(pl.h[c].alen, pl.h[c].blen) + 1);
-    }
-    if (pk) {
-      if ((st = gd_packed_bounds_launch(d_ch + c0, nc, d_roff + c0, pk->rowpos, max_rows, wsize, wstep, lo_a, hi_a,
-                                        lo_b, flags, sm)) ||
-          (st = gd_packed_snp_fet_launch(d_ch + c0, nc, d_woff + 2 * c0, pk->acodes, pk->bcodes, max_rows, binom,
-                                         ctx->lut_hdr, ctx->lut, snp, sm)))
-        return fail(st, "packed pass launch failed");
-    } else {
-      const int64_t epb = gd_bounds_elems_per_block();
-      const unsigned gxb = (unsigned)std::min<int64_t>((mx + epb - 1) / epb, std::max(1, 8192 / nc));
-      hipLaunchKernelGGL(k_bounds, dim3(gxb, nc, 2), dim3(256), 0, sm, d_ch + c0, apos, bpos, wsize, wstep, lo_a,
-                         hi_a, lo_b, flags);
-      const unsigned gxs = (unsigned)std::min<int64_t>((amax + 255) / 256, std::max(1, 8192 / nc));
-      hipLaunchKernelGGL(k_snp_fet, dim3(gxs, nc), dim3(256), 0, sm, d_ch + c0, avals, bvals, binom,
-                         ctx->lut_hdr, ctx->lut, snp, fused ? 1 : 0);
+  const char *fg = getenv("GD_FORCE_GENERAL"), *sv = getenv("GD_FET_SCHED");
+  const bool sched = fused && !(fg && fg[0] == '1') && (sv && sv[0] == '1');
+  /* GD_FET_B0=1: chromosome 0's bounds as a pass of their own before the window kernel */
+  const char *b0e = getenv("GD_FET_B0");
+  const bool b0 = sched && b0e && b0e[0] == '1';
+  std::vector<int32_t> bt_off(nchrom + 1, 0);
+  for (int c = 0; c < nchrom; ++c) {
+    const int64_t t = (pl.h[c].wend > 0 && !(b0 && c == 0))
+                          ? (int64_t)gd_fet_bounds_tiles(pl.h[c].alen) + gd_fet_bounds_tiles(pl.h[c].blen)
+                          : 0;
+    if ((int64_t)bt_off[c] + t > INT32_MAX) return fail(GD_ERR_SIZE, "batch too large for one scheduled scan");
+    bt_off[c + 1] = bt_off[c] + (int32_t)t;
+  }
+  blk_off.insert(blk_off.end(), bt_off.begin(), bt_off.end());
+  if ((st = h2d(ctx, d_blk, blk_off.data(), sizeof(int32_t) * blk_off.size(), s))) return st;
+  const int32_t *d_bt = d_blk + nchrom + 1;
+  HIP_TRY(hipMemsetAsync(flags, 0, nflags * sizeof(unsigned), s));
+  HIP_TRY(hipEventRecord(ctx->ev[0], s));
+  if (sched) {
+    hipLaunchKernelGGL(k_fet_setup, dim3(256), dim3(256), 0, s, d_ch, nchrom, apos, bpos, flags, binom, ctx->lut_hdr,
+                       ctx->lut, (int64_t)GD_LUT_CAP, flags + 12);
+    int64_t amax = 1;
+    for (int c = 0; c < nchrom; ++c) amax = std::max<int64_t>(amax, pl.h[c].alen);
+    const unsigned gxs = (unsigned)std::min<int64_t>((amax + 255) / 256, std::max(1, 1024 / nchrom));
+    hipLaunchKernelGGL(k_snp_fet, dim3(gxs, nchrom), dim3(256), 0, s, d_ch, avals, bvals, binom, ctx->lut_hdr,
+                       ctx->lut, snp, 1);
+    if (b0 && pl.h[0].wend > 0) {
+      const int64_t mx = std::max(pl.h[0].alen, pl.h[0].blen) + 1, epb = gd_bounds_elems_per_block();
+      hipLaunchKernelGGL(k_bounds, dim3((unsigned)std::min<int64_t>((mx + epb - 1) / epb, 8192), 1, 2), dim3(256), 0,
+                         s, d_ch, apos, bpos, wsize, wstep, lo_a, hi_a, lo_b, flags);
     }
     HIP_TRY(hipGetLastError());
-    HIP_TRY(hipEventRecord(ctx->gev[g], sm));
-  }
-  HIP_TRY(hipEventRecord(ctx->ev[1], sm));
-  /* with G > 1 the groups' window kernels alternate between stream2 and the caller's stream,
-   * so two of them run at once (their outputs are disjoint, the declined-window list and the
-   * flags atomic); GD_WALT=0 keeps them all on stream2 (diagnostics) */
-  const char *walt = getenv("GD_WALT");
-  const bool alt = G > 1 && !(walt && walt[0] == '0');
-  for (int g = 0; g < G && !force_general; ++g) {
-    const int c0 = cuts[g], c1 = cuts[g + 1];
-    hipStream_t sw = (alt && (g & 1)) ? s : s2;
-    if (G > 1) HIP_TRY(hipStreamWaitEvent(sw, ctx->gev[g], 0));
-    st = gd_fet_window_fast_launch(d_ch, nchrom, d_blk, blk_off[c0], blk_off[c1] - blk_off[c0], lo_a, hi_a, lo_b,
-                                   snp, avals, bvals, binom, ctx->lut_hdr, ctx->lut, fused ? 1 : 0, perc, scores,
-                                   stddev, flags, list, list_count, sw);
-    if (st) return fail(st, "fast window kernel launch failed");
-  }
-  HIP_TRY(hipEventRecord(ctx->ev[2], s2));
-  if (G > 1) {
-    HIP_TRY(hipStreamWaitEvent(s, ctx->ev[1], 0));
-    HIP_TRY(hipStreamWaitEvent(s, ctx->ev[2], 0));
+    HIP_TRY(hipEventRecord(ctx->ev[1], s));
+    int nb = 256;
+    if (const char *e = getenv("GD_FET_NB")) nb = std::max(0, atoi(e)); /* diagnostics */
+    gd_fet_sched sc;
+    std::memset(&sc, 0, sizeof sc);
+    sc.ticket = flags + 13;
+    sc.bdone = flags + 32;
+    sc.bt_off = d_bt;
+    sc.apos = apos;
+    sc.bpos = bpos;
+    sc.nb = (int)std::min<int64_t>(bt_off[nchrom], nb > 0 ? nb : 1);
+    sc.wsize = wsize;
+    sc.wstep = wstep;
+    sc.bstride = bstride;
+    sc.poll = 1;
+    if (const char *e = getenv("GD_FET_POLL")) sc.poll = std::max(1, atoi(e)); /* diagnostics */
+    if ((st = h2d(ctx, d_sc, &sc, sizeof sc, s))) return st;
+    if ((st = gd_fet_window_sched_launch(d_ch, nchrom, d_blk, blk_off[nchrom], lo_a, hi_a, lo_b, snp, avals, bvals,
+                                         binom, ctx->lut_hdr, ctx->lut, perc, scores, stddev, flags, list, list_count,
+                                         d_sc, sc.nb, s)))
+      return fail(st, "scheduled window kernel launch failed");
+    HIP_TRY(hipEventRecord(ctx->ev[2], s));
+  } else {
+    /* Pipeline over chromosome groups on the context's two streams: the HBM-bound
+     * passes (bounds + per-SNP FET) run on the high-priority stream and feed the
+     * VALU-bound bootstrap of each group on the low-priority stream as soon as the
+     * group's rows are scored.  The caller's stream `s` orders the scan against its
+     * other work. */
+    int G = std::min(nchrom, GD_DEFAULT_GROUPS);
+    if (const char *eg = getenv("GD_GROUPS")) G = std::max(1, std::min(std::min(nchrom, GD_MAX_GROUPS), atoi(eg))); /* diagnostics */
+    /* one group (the default): every kernel on the caller's stream, no cross-stream event waits
+     * between the passes */
+    hipStream_t sm = G > 1 ? ctx->stream_mem : s, s2 = G > 1 ? ctx->stream2 : s;
+    if (G > 1) HIP_TRY(hipStreamWaitEvent(sm, ctx->ev[0], 0));
+    if (!pk) hipLaunchKernelGGL(k_popsize, dim3(nchrom), dim3(64), 0, sm, d_ch, apos, bpos, flags);
+    bool force_general = false;
+    if ((st = gd_fet_window_prepare(pl.wtotal, list, list_count, sm, &force_general))) return st;
+    /* score table for chromosome 0's population sizes (no-op when cached) */
+    hipLaunchKernelGGL(k_fet_lut_build, dim3(512), dim3(256), 0, sm, d_ch, binom, ctx->lut_hdr, ctx->lut,
+                       (int64_t)GD_LUT_CAP);
+    hipLaunchKernelGGL(k_fet_lut_publish, dim3(1), dim3(1), 0, sm, d_ch, binom, ctx->lut_hdr, (int64_t)GD_LUT_CAP);
+
+    /* fused (default): wherever the score table holds a chromosome's sizes, the window
+     * kernel scores its own span rows from the genotype values and the per-SNP pass
+     * (k_snp_fet) exits at once, so the only full pass is k_bounds; GD_FET_UNFUSED=1
+     * restores the per-SNP pass feeding the window kernel through snp_score */
+    std::vector<int> cuts(G + 1);
+    for (int g = 0; g <= G; ++g) cuts[g] = (int)((int64_t)nchrom * g / G);
+    for (int g = 0; g < G; ++g) {
+      const int c0 = cuts[g], nc = cuts[g + 1] - cuts[g];
+      if (nc <= 0) continue;
+      int64_t amax = 1, mx = 1;
+      for (int c = c0; c < c0 + nc; ++c) {
+        amax = std::max<int64_t>(amax, pl.h[c].alen);
+        mx = std::max<int64_t>(mx, std::max(pl.h[c].alen, pl.h[c].blen) + 1);
+      }
+      if (pk) {
+        if ((st = gd_packed_bounds_launch(d_ch + c0, nc, d_roff + c0, pk->rowpos, max_rows, wsize, wstep, lo_a, hi_a,
+                                          lo_b, flags, sm)) ||
+            (st = gd_packed_snp_fet_launch(d_ch + c0, nc, d_woff + 2 * c0, pk->acodes, pk->bcodes, max_rows, binom,
+                                           ctx->lut_hdr, ctx->lut, snp, sm)))
+          return fail(st, "packed pass launch failed");
+      } else {
+        const int64_t epb = gd_bounds_elems_per_block();
+        const unsigned gxb = (unsigned)std::min<int64_t>((mx + epb - 1) / epb, std::max(1, 8192 / nc));
+        hipLaunchKernelGGL(k_bounds, dim3(gxb, nc, 2), dim3(256), 0, sm, d_ch + c0, apos, bpos, wsize, wstep, lo_a,
+                           hi_a, lo_b, flags);
+        const unsigned gxs = (unsigned)std::min<int64_t>((amax + 255) / 256, std::max(1, 8192 / nc));
+        hipLaunchKernelGGL(k_snp_fet, dim3(gxs, nc), dim3(256), 0, sm, d_ch + c0, avals, bvals, binom,
+                           ctx->lut_hdr, ctx->lut, snp, fused ? 1 : 0);
+      }
+      HIP_TRY(hipGetLastError());
+      HIP_TRY(hipEventRecord(ctx->gev[g], sm));
+    }
+    HIP_TRY(hipEventRecord(ctx->ev[1], sm));
+    /* with G > 1 the groups' window kernels alternate between stream2 and the caller's stream,
+     * so two of them run at once (their outputs are disjoint, the declined-window list and the
+     * flags atomic); GD_WALT=0 keeps them all on stream2 (diagnostics) */
+    const char *walt = getenv("GD_WALT");
+    const bool alt = G > 1 && !(walt && walt[0] == '0');
+    for (int g = 0; g < G && !force_general; ++g) {
+      const int c0 = cuts[g], c1 = cuts[g + 1];
+      hipStream_t sw = (alt && (g & 1)) ? s : s2;
+      if (G > 1) HIP_TRY(hipStreamWaitEvent(sw, ctx->gev[g], 0));
+      st = gd_fet_window_fast_launch(d_ch, nchrom, d_blk, blk_off[c0], blk_off[c1] - blk_off[c0], lo_a, hi_a, lo_b,
+                                     snp, avals, bvals, binom, ctx->lut_hdr, ctx->lut, fused ? 1 : 0, perc, scores,
+                                     stddev, flags, list, list_count, sw);
+      if (st) return fail(st, "fast window kernel launch failed");
+    }
+    if (G > 1) {
+      /* ev[2] after every group's window kernel: the odd groups ran on s, the others on s2 */
+      HIP_TRY(hipEventRecord(ctx->ev[4], s2));
+      HIP_TRY(hipStreamWaitEvent(s, ctx->ev[4], 0));
+      HIP_TRY(hipStreamWaitEvent(s, ctx->ev[1], 0));
+    }
+    HIP_TRY(hipEventRecord(ctx->ev[2], s));
   }
   {
     /* windows the fast path declined: literal one-workgroup-per-window path */
@@ -579,8 +676,10 @@ static int fet_scan_locked(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, cons
     HIP_TRY(hipStreamSynchronize(s));
   }
   float ms;
-  /* stage times on the scan's streams: memory passes, end of the bootstrap, end of
-   * the general path, all measured from the scan's first kernel */
+  /* stage times (HIP events from the scan's first kernel): MEM = the prologue (scheduled
+   * scan: setup, per-SNP pass; grouped: every group's bounds / per-SNP passes), WINDOW = the
+   * end of the last fast window kernel (scheduled: incl. the bounds workers), GENERAL = the
+   * literal path after it, TOTAL */
   if (hipEventElapsedTime(&ms, ctx->ev[0], ctx->ev[1]) == hipSuccess) g_stage_ms[GD_STAGE_MEM] = ms;
   if (hipEventElapsedTime(&ms, ctx->ev[0], ctx->ev[2]) == hipSuccess) g_stage_ms[GD_STAGE_WINDOW] = ms;
   if (hipEventElapsedTime(&ms, ctx->ev[2], ctx->ev[3]) == hipSuccess) g_stage_ms[GD_STAGE_GENERAL] = ms;

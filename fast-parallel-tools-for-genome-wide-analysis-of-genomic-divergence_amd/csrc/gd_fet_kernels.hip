@@ -15,6 +15,7 @@
  * All FP arithmetic is compiled with -ffp-contract=off (the reference build has no FMA).
  */
 #include "gd_common.h"
+#include "gd_bounds.h"
 #include "gd_fet_rows.h"
 #include "gd_internal.h"
 
@@ -48,183 +49,46 @@ __global__ void k_binom_table(uint64_t *tab) {
 }
 
 /* get_population_size(): leading run of pos[0], bounded by the array length */
-__global__ void __launch_bounds__(64) k_popsize(gd_chrom_dev *ch, const int32_t *apos, const int32_t *bpos,
-                                                unsigned *flags) {
-  gd_chrom_dev &d = ch[blockIdx.x];
-  const int lane = threadIdx.x;
-  int sizes[2];
-  for (int pop = 0; pop < 2; ++pop) {
-    const int32_t *p = pop ? bpos + d.b_off : apos + d.a_off;
-    const int len = pop ? d.blen : d.alen;
-    int size = len;
-    if (len > 0) {
-      const int32_t p0 = p[0];
-      for (int base = 0; base < len; base += 64) {
-        const int i = base + lane;
-        const unsigned long long m = __ballot(i < len && p[i] != p0);
-        if (m) {
-          size = base + __ffsll((long long)m) - 1;
-          break;
-        }
-      }
-    }
-    sizes[pop] = size;
-  }
-  if (lane == 0) {
-    d.asize = sizes[0];
-    d.bsize = sizes[1];
+__device__ __forceinline__ void popsize_store(gd_chrom_dev &d, const int32_t *apos, const int32_t *bpos,
+                                              unsigned *flags) {
+  const int sa = gd_popsize_wave(apos + d.a_off, d.alen), sb = gd_popsize_wave(bpos + d.b_off, d.blen);
+  if ((threadIdx.x & 63) == 0) {
+    d.asize = sa;
+    d.bsize = sb;
     d.nrows = 0;
-    if (d.wend > 0 && (sizes[0] <= 0 || sizes[1] <= 0)) atomicOr(flags, GD_FLAG_BAD_SIZE);
-    if (sizes[0] > 0 && sizes[1] > 0) {
-      const int ra = d.alen / sizes[0], rb = d.blen / sizes[1];
+    if (d.wend > 0 && (sa <= 0 || sb <= 0)) atomicOr(flags, GD_FLAG_BAD_SIZE);
+    if (sa > 0 && sb > 0) {
+      const int ra = d.alen / sa, rb = d.blen / sb;
       d.nrows = ra < rb ? ra : rb;
     }
   }
 }
 
-/* floor(a / b) for b > 0, |a| < 2^40: double-reciprocal estimate, one fix-up step */
-__device__ __forceinline__ int64_t fdiv_fast(int64_t a, int32_t b, double inv) {
-  int64_t q = (int64_t)floor((double)a * inv);
-  const int64_t r = a - q * (int64_t)b;
-  q += (r >= b) - (r < 0);
-  return q;
+__global__ void __launch_bounds__(64) k_popsize(gd_chrom_dev *ch, const int32_t *apos, const int32_t *bpos,
+                                                unsigned *flags) {
+  popsize_store(ch[blockIdx.x], apos, bpos, flags);
 }
 
-/* slide_right() for all windows: lo = first idx with pos >= start,
- * hi = first idx with pos > start + wsize (inclusive end).  Grid (x, chrom, pop).
- * Element i owns the windows whose start lies in (pos[i-1], pos[i]] (lo) and whose
- * inclusive stop lies in [pos[i-1], pos[i]) (hi); i == len is the +inf sentinel.
- * Within a SNP's run of identical positions nothing is owned, so the common case
- * is one compare; each thread takes 4 consecutive elements. */
-__global__ void __launch_bounds__(256) k_bounds(const gd_chrom_dev *ch, const int32_t *apos, const int32_t *bpos,
-                                                int wsize, int wstep, int32_t *lo_a, int32_t *hi_a,
-                                                int32_t *lo_b, unsigned *flags) {
-  const gd_chrom_dev &d = ch[blockIdx.y];
-  const int pop = blockIdx.z;
-  const int64_t wend = d.wend;
-  if (wend <= 0) return;
-  const int64_t len = pop ? d.blen : d.alen;
-  const int32_t *pos = pop ? bpos + d.b_off : apos + d.a_off;
-  int32_t *lo = (pop ? lo_b : lo_a) + d.w_base;
-  int32_t *hi = hi_a + d.w_base;
-  const double inv = 1.0 / (double)wstep;
-  /* floor(a / wstep) for 0 <= a < 2^31 as a multiply-high (Granlund-Montgomery, N = 31:
-   * mag = ceil(2^(31+l) / wstep), l = ceil(log2 wstep)); other a (negative near the
-   * chromosome start, wstep == 1) take fdiv_fast */
-  int kl = 0;
-  while ((1ll << kl) < wstep) ++kl;
-  const uint32_t kmag = kl > 0 ? (uint32_t)(((1ull << (31 + kl)) + (uint64_t)wstep - 1) / (uint64_t)wstep) : 0u;
-  const uint32_t ksh = kl > 0 ? (uint32_t)(kl - 1) : 0u;
-  auto fl = [&](int64_t a) -> int64_t {
-    if (kl > 0 && a >= 0 && a < 0x80000000ll) return (int64_t)(__umulhi((uint32_t)a, kmag) >> ksh);
-    return fdiv_fast(a, wstep, inv);
-  };
-  const bool aligned16 = ((pop ? d.b_off : d.a_off) & 3) == 0; /* int4 loads stay 16-byte aligned */
-  /* each lane scans 4 KB_CH elements: bit k of `bits` marks a boundary (i == 0, i == len, or pos[i] != pos[i-1]; three
-   * VALU per element: unsigned difference, min with 1, shift-or), then the lane walks
-   * just those bits: a wave runs the window-range code max-boundaries-per-lane times
-   * (~1-2 at 20 individuals), not once per element */
-  /* a wave scans a KB_SEG-element segment (KB_CH chunks of 256): lane l's chunk k holds elements seg + 256 k + 4 l
-   * .. + 3 (one coalesced int4 per chunk: consecutive lanes read consecutive 16 bytes);
-   * an element's predecessor is the previous element of its chunk, or the last element of
-   * lane l - 1's chunk (ds_bpermute), or of lane 63's previous chunk.  The partial last
-   * segment takes the element-by-element path (4 KB_CH consecutive elements per lane). */
+/* slide_right() for all windows (gd_bounds.h).  Grid (x, chrom, pop); a wave scans
+ * KB_SEG-element segments grid-strided, reading each segment with KB_CH coalesced int4
+ * loads per lane. */
 #ifndef KB_CH
 #define KB_CH 4 /* int4 chunks per lane and segment (loads in flight; 4: 0.326 ms per C2 bounds pass, 8: 0.312 (parity not yet run on the GPU), 2: 0.366) */
 #endif
-  static_assert(KB_CH >= 1 && 4 * KB_CH <= 32, "the boundary mask holds 4 KB_CH bits in a uint32_t");
+__global__ void __launch_bounds__(256) k_bounds(const gd_chrom_dev *ch, const int32_t *apos, const int32_t *bpos,
+                                                int wsize, int wstep, int32_t *lo_a, int32_t *hi_a,
+                                                int32_t *lo_b, unsigned *flags) {
   constexpr int KB_SEG = 256 * KB_CH;
-#ifndef KB_LDS
-#define KB_LDS 1
-#endif
-#if KB_LDS
   __shared__ __attribute__((aligned(16))) int32_t kb_sh[4][KB_SEG];
-#endif
-  const int lane = threadIdx.x & 63;
+  const gd_chrom_dev &d = ch[blockIdx.y];
+  if (d.wend <= 0) return;
+  const gd_bounds_job job(d, blockIdx.z, apos, bpos, wsize, wstep, lo_a, hi_a, lo_b);
   const int64_t wave0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
   bool unsorted = false;
-  /* element i (a boundary: i == 0, i == len or pos[i] != pos[i-1]) with p = pos[i] (i < len)
-   * and pp = pos[i-1] (i > 0) */
-  auto own = [&](int64_t i, int64_t p, int64_t pp) {
-    const bool first = (i == 0), last = (i == len);
-    int64_t f = first ? 0 : fl(pp) + 1;
-    int64_t l = last ? wend - 1 : fl(p);
-    if (f < 0) f = 0;
-    if (l > wend - 1) l = wend - 1;
-    for (int64_t w = f; w <= l; ++w) lo[w] = (int32_t)i;
-    if (pop == 0) {
-      /* -floor((wsize - x) / wstep) = ceil((x - wsize) / wstep) = floor((x - wsize + wstep - 1) / wstep) */
-      f = first ? 0 : fl(pp - wsize + wstep - 1);
-      l = last ? wend - 1 : fl(p - wsize + wstep - 1) - 1;
-      if (f < 0) f = 0;
-      if (l > wend - 1) l = wend - 1;
-      for (int64_t w = f; w <= l; ++w) hi[w] = (int32_t)i;
-    }
-  };
-  for (int64_t seg = wave0 * KB_SEG; seg <= len; seg += nwaves * KB_SEG) {
-    if (aligned16 && seg + KB_SEG <= len) {
-      int4 v[KB_CH];
-#pragma unroll
-      for (int k = 0; k < KB_CH; ++k) v[k] = *reinterpret_cast<const int4 *>(pos + seg + 256 * k + 4 * lane);
-      const int32_t before = seg > 0 ? pos[seg - 1] : v[0].x; /* element 0 has no predecessor */
-      uint32_t bits = 0;
-      bool dec = false;
-#pragma unroll
-      for (int k = 0; k < KB_CH; ++k) {
-        const int32_t up = __shfl_up(v[k].w, 1);
-        const int32_t wrap = __shfl(v[k > 0 ? k - 1 : 0].w, 63);
-        const int32_t prev = lane > 0 ? up : (k > 0 ? wrap : before);
-        const int32_t e[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
-        int32_t pv = prev;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          bits |= min((uint32_t)e[j] - (uint32_t)pv, 1u) << (4 * k + j);
-          dec |= e[j] < pv;
-          pv = e[j];
-        }
-      }
-      if (seg == 0 && lane == 0) bits |= 1u; /* element 0 opens the first run */
-      unsorted |= dec;
-#if KB_LDS
-      /* the segment in element order in the wave's LDS slice: the boundary walk reads
-       * pos[i] and pos[i - 1] from there instead of going back to memory */
-      int32_t *sg = kb_sh[threadIdx.x >> 6];
-#pragma unroll
-      for (int k = 0; k < KB_CH; ++k) *reinterpret_cast<int4 *>(sg + 256 * k + 4 * lane) = v[k];
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      while (bits) {
-        const int b = __builtin_ctz(bits);
-        bits &= bits - 1;
-        const int r = 256 * (b >> 2) + 4 * lane + (b & 3);
-        own(seg + r, sg[r], r > 0 ? sg[r - 1] : before);
-      }
-      __builtin_amdgcn_wave_barrier(); /* the slice is rewritten by the next segment */
-#else
-      while (bits) {
-        const int b = __builtin_ctz(bits);
-        bits &= bits - 1;
-        const int64_t i = seg + 256 * (b >> 2) + 4 * lane + (b & 3);
-        own(i, pos[i], i > 0 ? pos[i - 1] : 0);
-      }
-#endif
-    } else {
-      for (int64_t i0 = seg + 4 * KB_CH * lane; i0 < seg + KB_SEG && i0 <= len; i0 += KB_SEG) {
-        int32_t prev = (i0 > 0) ? pos[i0 - 1] : 0;
-        for (int k = 0; k < 4 * KB_CH && i0 + k <= len; ++k) {
-          const int64_t i = i0 + k;
-          const int32_t v = (i < len) ? pos[i] : 0;
-          const bool bnd = (i == 0) || (i == len) || (v != prev);
-          if (i > 0 && i < len) unsorted |= (v < prev);
-          if (bnd) own(i, v, prev);
-          prev = v;
-        }
-      }
-    }
-  }
-  if (unsorted) atomicOr(flags, pop ? GD_FLAG_UNSORTED_B : GD_FLAG_UNSORTED_A);
+  for (int64_t seg = wave0 * KB_SEG; seg <= job.len; seg += nwaves * KB_SEG)
+    unsorted |= job.segment<KB_CH>(seg, kb_sh[threadIdx.x >> 6]);
+  if (unsorted) atomicOr(flags, job.pop ? GD_FLAG_UNSORTED_B : GD_FLAG_UNSORTED_A);
 }
 
 /* ------------------------------------------------------------------------ */
@@ -339,6 +203,58 @@ __global__ void k_fet_lut_publish(const gd_chrom_dev *ch, const uint64_t *binom,
   hdr[1] = bsize;
   hdr[2] = ok ? 1 : 0;
   hdr[3] = fet_mode(binom);
+}
+
+/* The prologue of a scheduled FET scan in one launch (gd_api.hip): every chromosome's
+ * population sizes (one wave each, as k_popsize), the score table for chromosome 0's sizes
+ * when the context does not hold it yet (as k_fet_lut_build; every workgroup derives the
+ * sizes itself from the positions, so nothing waits for the size pass), and the header,
+ * written by the last workgroup to finish (done: a zeroed counter).  With the table
+ * cached the launch only reads a few positions per chromosome. */
+__global__ void __launch_bounds__(256) k_fet_setup(gd_chrom_dev *ch, int nchrom, const int32_t *apos,
+                                                   const int32_t *bpos, unsigned *flags, const uint64_t *binom,
+                                                   int *hdr, double *lut, int64_t cap, unsigned *done) {
+  __shared__ int sh_sz[2];
+  const int wave = threadIdx.x >> 6;
+  if (wave == 0) {
+    const gd_chrom_dev &d0 = ch[0];
+    const int sa = gd_popsize_wave(apos + d0.a_off, d0.alen), sb = gd_popsize_wave(bpos + d0.b_off, d0.blen);
+    if (threadIdx.x == 0) {
+      sh_sz[0] = sa;
+      sh_sz[1] = sb;
+    }
+  }
+  for (int c = blockIdx.x * 4 + wave; c < nchrom; c += gridDim.x * 4) popsize_store(ch[c], apos, bpos, flags);
+  __syncthreads();
+  const int asize = sh_sz[0], bsize = sh_sz[1];
+  const int64_t na = (int64_t)(asize + 1) * (asize + 2) / 2, nb = (int64_t)(bsize + 1) * (bsize + 2) / 2;
+  const bool ok = asize > 0 && bsize > 0 && na * nb <= cap;
+  const bool cached = hdr[2] == 1 && hdr[0] == asize && hdr[1] == bsize && hdr[3] == fet_mode(binom);
+  if (ok && !cached) {
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < na * nb;
+         e += (int64_t)gridDim.x * blockDim.x) {
+      int ia = (int)(e / nb), ib = (int)(e - (int64_t)ia * nb);
+      int a = 0, c = 0;
+      while (ia >= asize + 1 - a) {
+        ia -= asize + 1 - a;
+        ++a;
+      }
+      while (ib >= bsize + 1 - c) {
+        ib -= bsize + 1 - c;
+        ++c;
+      }
+      lut[e] = gd_fet_score_from_p(fet_p_two_tailed(a, ia, c, ib, binom));
+    }
+  }
+  /* the table and the header are read by later kernels only (kernel-boundary ordering): the
+   * counter just picks the workgroup that writes the header after every slice is built */
+  __syncthreads();
+  if (threadIdx.x == 0 && atomicAdd(done, 1u) == gridDim.x - 1) {
+    hdr[0] = asize;
+    hdr[1] = bsize;
+    hdr[2] = ok ? 1 : 0;
+    hdr[3] = fet_mode(binom);
+  }
 }
 
 /* ------------------------------------------------------------------------ */

@@ -1,11 +1,11 @@
 #!/bin/bash
 # Build an A/B variant of libgdscan.so: csrc/gd_css_kernels.hip (or $SRC) recompiled with
 # extra flags, linked with the other objects of the regular build.
-# usage: tools/build_variant.sh NAME "-DGD_CSS_PROFILE ..."   -> tools/ab/NAME/libgdscan.so (git-ignored; delete after the A/B session: it travels with every gpurun call)
+# usage: tools/build_variant.sh NAME "-DGD_CSS_PROFILE ..."   -> varlib/NAME/libgdscan.so (git-ignored; delete after the A/B session: it travels with every gpurun call)
 set -e
 NAME=$1; FLAGS=$2; SRC=${SRC:-gd_css_kernels}
 P=$(cd "$(dirname "$0")/.." && pwd)/fast-parallel-tools-for-genome-wide-analysis-of-genomic-divergence_amd
-OUT=$(dirname "$0")/ab/$NAME
+OUT=$(cd "$(dirname "$0")/.." && pwd)/varlib/$NAME
 mkdir -p "$OUT"
 make -s -C "$P" >/dev/null
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -w $FLAGS \
