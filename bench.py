@@ -170,7 +170,8 @@ def fet_cpu_baseline(args, scores_dev, chroms):
     total_t = 0.0
     nwin = exact = 0
     max_rel = 0.0
-    for c in range(args.cpu_chroms):
+    ncpu = min(args.cpu_chroms, len(chroms))
+    for c in range(ncpu):
         av, bv, ap_, bp, regend = synth.chromosome(c, args.nsnp, args.asize, args.bsize)
         n = regend // args.wstep
         s, d = np.zeros(n), np.zeros(n)
@@ -196,7 +197,7 @@ def fet_cpu_baseline(args, scores_dev, chroms):
         "value": total_w / total_t, "unit": "windows/s", "cores": min(threads, usable), "kind": kind,
         "parity_windows": nwin, "parity_bit_exact_frac": exact / max(nwin, 1), "parity_max_rel": max_rel,
         "threads": threads, "cpu_model": model,
-        "sample": f"{args.cpu_chroms}/{args.nchrom} chromosomes, {total_w} windows in {total_t:.2f} s"
+        "sample": f"{ncpu}/{args.nchrom} chromosomes, {total_w} windows in {total_t:.2f} s"
                   + (f", reference threadcompute, 64 pthreads on {min(64, usable)} cores" if kind == "reference"
                      else ", oracle, 1 thread"),
         "what": f"{kind} {'threadcompute (oracle/_ref, built from the reference sources)' if kind == 'reference' else 'orc_fet_scan'}"

@@ -55,12 +55,6 @@ int gd_pack_device_launch(const double *avals, const double *bvals, const int32_
 int gd_fet_fast_windows_per_block();
 __global__ void k_fet_setup(gd_chrom_dev *ch, int nchrom, const int32_t *apos, const int32_t *bpos, unsigned *flags,
                             const uint64_t *binom, int *hdr, double *lut, int64_t cap, unsigned *done);
-int gd_fet_window_sched_launch(const gd_chrom_dev *ch, int nchrom, const int32_t *blk_off, int blk_count,
-                               int32_t *lo_a, int32_t *hi_a, int32_t *lo_b, const double *snp_score,
-                               const double *avals, const double *bvals, const uint64_t *binom, const int *lut_hdr,
-                               const double *lut, double perc, double *scores, double *stddev, unsigned *flags,
-                               int32_t *slow_list, unsigned *slow_count, const gd_fet_sched *d_sc, int nb,
-                               hipStream_t s);
 int gd_bounds_elems_per_block();
 int gd_fet_fast_init(hipStream_t s);
 int gd_fet_window_prepare(int64_t wtotal, int32_t *slow_list, unsigned *slow_count, hipStream_t s,
@@ -461,15 +455,12 @@ static int fet_scan_locked(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, cons
 
   Carve cv{nullptr};
   /* flags: [0] status bits, [4] declined-window count, [8] dense-window count, [12] the
-   * setup kernel's done counter, [13] the window kernel's ticket, [32 + bstride c]
-   * chromosome c's bounds tiles written (scheduled scan) -- all zeroed by one memset */
-  int bstride = 32; /* one 128-byte line per chromosome's counter */
-  if (const char *e = getenv("GD_FET_BSTRIDE")) bstride = std::max(1, atoi(e)); /* diagnostics */
-  const size_t nflags = 32 + (size_t)nchrom * bstride;
+   * setup kernel's done counter -- zeroed by one memset per scan */
+  const size_t nflags = 16;
   auto layout = [&](Carve &k, gd_chrom_dev **d_ch, int32_t **d_blk, unsigned **flags, int32_t **lo_a,
                     int32_t **hi_a, int32_t **lo_b, double **snp, int32_t **list, int32_t **huge) {
     *d_ch = k.take<gd_chrom_dev>(nchrom);
-    *d_blk = k.take<int32_t>(2 * (size_t)nchrom + 2); /* workgroup offsets, then bounds-tile offsets */
+    *d_blk = k.take<int32_t>(nchrom + 1);
     *flags = k.take<unsigned>(nflags);
     *lo_a = k.take<int32_t>(pl.wtotal);
     *hi_a = k.take<int32_t>(pl.wtotal);
@@ -478,7 +469,6 @@ static int fet_scan_locked(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, cons
     *list = k.take<int32_t>(pl.wtotal);
     *huge = k.take<int32_t>(pl.wtotal);
   };
-  gd_fet_sched *d_sc = nullptr;
   gd_chrom_dev *d_ch;
   unsigned *flags;
   int32_t *d_blk, *lo_a, *hi_a, *lo_b, *list, *huge;
@@ -486,7 +476,6 @@ static int fet_scan_locked(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, cons
   int64_t *d_roff = nullptr, *d_woff = nullptr;
   auto layout_all = [&](Carve &k) {
     layout(k, &d_ch, &d_blk, &flags, &lo_a, &hi_a, &lo_b, &snp, &list, &huge);
-    d_sc = k.take<gd_fet_sched>(1);
     if (pk) {
       d_roff = k.take<int64_t>(nchrom);
       d_woff = k.take<int64_t>(2 * (size_t)nchrom);
@@ -503,143 +492,103 @@ static int fet_scan_locked(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, cons
     if ((st = h2d(ctx, d_woff, word_off.data(), sizeof(int64_t) * 2 * nchrom, s))) return st;
   }
   if ((st = h2d(ctx, d_ch, pl.h.data(), sizeof(gd_chrom_dev) * nchrom, s))) return st;
-  /* Scheduled scan (the default for reference-layout tracks): one stream, three launches --
-   * k_fet_setup (sizes, score table), the per-SNP pass (exits at once wherever the table
-   * holds the sizes), and the window kernel, whose first workgroups run the bounds pass
-   * chromosome by chromosome while the others bootstrap the windows whose bounds are done
-   * (gd_fet_fast.hip).  Opt-in while it is tuned (GD_FET_SCHED=1); the grouped two-stream
-   * pipeline below is the default. */
-  const char *uf = getenv("GD_FET_UNFUSED");
-  const bool fused = !pk && !(uf && uf[0] == '1'); /* packed: the per-SNP pass reads 2 bits per genotype */
-  const char *fg = getenv("GD_FORCE_GENERAL"), *sv = getenv("GD_FET_SCHED");
-  const bool sched = fused && !(fg && fg[0] == '1') && (sv && sv[0] == '1');
-  /* GD_FET_B0=1: chromosome 0's bounds as a pass of their own before the window kernel */
-  const char *b0e = getenv("GD_FET_B0");
-  const bool b0 = sched && b0e && b0e[0] == '1';
-  std::vector<int32_t> bt_off(nchrom + 1, 0);
-  for (int c = 0; c < nchrom; ++c) {
-    const int64_t t = (pl.h[c].wend > 0 && !(b0 && c == 0))
-                          ? (int64_t)gd_fet_bounds_tiles(pl.h[c].alen) + gd_fet_bounds_tiles(pl.h[c].blen)
-                          : 0;
-    if ((int64_t)bt_off[c] + t > INT32_MAX) return fail(GD_ERR_SIZE, "batch too large for one scheduled scan");
-    bt_off[c + 1] = bt_off[c] + (int32_t)t;
-  }
-  blk_off.insert(blk_off.end(), bt_off.begin(), bt_off.end());
-  if ((st = h2d(ctx, d_blk, blk_off.data(), sizeof(int32_t) * blk_off.size(), s))) return st;
-  const int32_t *d_bt = d_blk + nchrom + 1;
+  if ((st = h2d(ctx, d_blk, blk_off.data(), sizeof(int32_t) * (nchrom + 1), s))) return st;
   HIP_TRY(hipMemsetAsync(flags, 0, nflags * sizeof(unsigned), s));
   HIP_TRY(hipEventRecord(ctx->ev[0], s));
-  if (sched) {
-    hipLaunchKernelGGL(k_fet_setup, dim3(256), dim3(256), 0, s, d_ch, nchrom, apos, bpos, flags, binom, ctx->lut_hdr,
+  /* Pipeline over chromosome groups: the passes (prologue, then each group's bounds) run in
+   * order on the high-priority stream sm; group g's window kernel waits for its own bounds
+   * pass only, the window kernels alternating between stream2 and the caller's stream s so
+   * that one starts while the other drains.  Two equal groups (r05 sweep, C2 per scan: 2
+   * groups 2.216-2.227 ms, 1 group 2.253, 3 groups 2.299; doubling groups 1, 2, 4, ... with
+   * the later bounds passes at one workgroup per CU 2.230-2.238, on the whole GPU 2.357-2.392;
+   * the same with the window kernels' LDS padded to six workgroups per CU, so that a bounds
+   * workgroup always fits beside them, 2.300-2.312).  A pass that runs beside a window kernel
+   * displaces window workgroups (LDS, VGPRs and wave slots are all but full at seven per CU),
+   * so it costs its own slot-time wherever it is scheduled: the bounds pass is hidden only
+   * for the second group's share.  (GD_GROUPS=<n>: diagnostics.) */
+  const char *uf = getenv("GD_FET_UNFUSED");
+  const bool fused = !pk && !(uf && uf[0] == '1'); /* packed: the per-SNP pass reads 2 bits per genotype */
+  int G = std::min(nchrom, 2);
+  if (const char *eg = getenv("GD_GROUPS")) G = std::max(1, std::min(std::min(nchrom, GD_MAX_GROUPS), atoi(eg)));
+  hipStream_t sm = G > 1 ? ctx->stream_mem : s, s2 = G > 1 ? ctx->stream2 : s;
+  if (G > 1) HIP_TRY(hipStreamWaitEvent(sm, ctx->ev[0], 0));
+  bool force_general = false;
+  if ((st = gd_fet_window_prepare(pl.wtotal, list, list_count, sm, &force_general))) return st;
+  if (!pk) {
+    /* population sizes and the score table for chromosome 0's sizes in one launch (the table
+     * build is a no-op when the context holds it) */
+    hipLaunchKernelGGL(k_fet_setup, dim3(256), dim3(256), 0, sm, d_ch, nchrom, apos, bpos, flags, binom, ctx->lut_hdr,
                        ctx->lut, (int64_t)GD_LUT_CAP, flags + 12);
-    int64_t amax = 1;
-    for (int c = 0; c < nchrom; ++c) amax = std::max<int64_t>(amax, pl.h[c].alen);
-    const unsigned gxs = (unsigned)std::min<int64_t>((amax + 255) / 256, std::max(1, 1024 / nchrom));
-    hipLaunchKernelGGL(k_snp_fet, dim3(gxs, nchrom), dim3(256), 0, s, d_ch, avals, bvals, binom, ctx->lut_hdr,
-                       ctx->lut, snp, 1);
-    if (b0 && pl.h[0].wend > 0) {
-      const int64_t mx = std::max(pl.h[0].alen, pl.h[0].blen) + 1, epb = gd_bounds_elems_per_block();
-      hipLaunchKernelGGL(k_bounds, dim3((unsigned)std::min<int64_t>((mx + epb - 1) / epb, 8192), 1, 2), dim3(256), 0,
-                         s, d_ch, apos, bpos, wsize, wstep, lo_a, hi_a, lo_b, flags);
-    }
-    HIP_TRY(hipGetLastError());
-    HIP_TRY(hipEventRecord(ctx->ev[1], s));
-    int nb = 256;
-    if (const char *e = getenv("GD_FET_NB")) nb = std::max(0, atoi(e)); /* diagnostics */
-    gd_fet_sched sc;
-    std::memset(&sc, 0, sizeof sc);
-    sc.ticket = flags + 13;
-    sc.bdone = flags + 32;
-    sc.bt_off = d_bt;
-    sc.apos = apos;
-    sc.bpos = bpos;
-    sc.nb = (int)std::min<int64_t>(bt_off[nchrom], nb > 0 ? nb : 1);
-    sc.wsize = wsize;
-    sc.wstep = wstep;
-    sc.bstride = bstride;
-    sc.poll = 1;
-    if (const char *e = getenv("GD_FET_POLL")) sc.poll = std::max(1, atoi(e)); /* diagnostics */
-    if ((st = h2d(ctx, d_sc, &sc, sizeof sc, s))) return st;
-    if ((st = gd_fet_window_sched_launch(d_ch, nchrom, d_blk, blk_off[nchrom], lo_a, hi_a, lo_b, snp, avals, bvals,
-                                         binom, ctx->lut_hdr, ctx->lut, perc, scores, stddev, flags, list, list_count,
-                                         d_sc, sc.nb, s)))
-      return fail(st, "scheduled window kernel launch failed");
-    HIP_TRY(hipEventRecord(ctx->ev[2], s));
   } else {
-    /* Pipeline over chromosome groups on the context's two streams: the HBM-bound
-     * passes (bounds + per-SNP FET) run on the high-priority stream and feed the
-     * VALU-bound bootstrap of each group on the low-priority stream as soon as the
-     * group's rows are scored.  The caller's stream `s` orders the scan against its
-     * other work. */
-    int G = std::min(nchrom, GD_DEFAULT_GROUPS);
-    if (const char *eg = getenv("GD_GROUPS")) G = std::max(1, std::min(std::min(nchrom, GD_MAX_GROUPS), atoi(eg))); /* diagnostics */
-    /* one group (the default): every kernel on the caller's stream, no cross-stream event waits
-     * between the passes */
-    hipStream_t sm = G > 1 ? ctx->stream_mem : s, s2 = G > 1 ? ctx->stream2 : s;
-    if (G > 1) HIP_TRY(hipStreamWaitEvent(sm, ctx->ev[0], 0));
-    if (!pk) hipLaunchKernelGGL(k_popsize, dim3(nchrom), dim3(64), 0, sm, d_ch, apos, bpos, flags);
-    bool force_general = false;
-    if ((st = gd_fet_window_prepare(pl.wtotal, list, list_count, sm, &force_general))) return st;
-    /* score table for chromosome 0's population sizes (no-op when cached) */
     hipLaunchKernelGGL(k_fet_lut_build, dim3(512), dim3(256), 0, sm, d_ch, binom, ctx->lut_hdr, ctx->lut,
                        (int64_t)GD_LUT_CAP);
     hipLaunchKernelGGL(k_fet_lut_publish, dim3(1), dim3(1), 0, sm, d_ch, binom, ctx->lut_hdr, (int64_t)GD_LUT_CAP);
-
-    /* fused (default): wherever the score table holds a chromosome's sizes, the window
-     * kernel scores its own span rows from the genotype values and the per-SNP pass
-     * (k_snp_fet) exits at once, so the only full pass is k_bounds; GD_FET_UNFUSED=1
-     * restores the per-SNP pass feeding the window kernel through snp_score */
-    std::vector<int> cuts(G + 1);
-    for (int g = 0; g <= G; ++g) cuts[g] = (int)((int64_t)nchrom * g / G);
-    for (int g = 0; g < G; ++g) {
-      const int c0 = cuts[g], nc = cuts[g + 1] - cuts[g];
-      if (nc <= 0) continue;
-      int64_t amax = 1, mx = 1;
-      for (int c = c0; c < c0 + nc; ++c) {
-        amax = std::max<int64_t>(amax, pl.h[c].alen);
-        mx = std::max<int64_t>(mx, std::max(pl.h[c].alen, pl.h[c].blen) + 1);
-      }
-      if (pk) {
-        if ((st = gd_packed_bounds_launch(d_ch + c0, nc, d_roff + c0, pk->rowpos, max_rows, wsize, wstep, lo_a, hi_a,
-                                          lo_b, flags, sm)) ||
-            (st = gd_packed_snp_fet_launch(d_ch + c0, nc, d_woff + 2 * c0, pk->acodes, pk->bcodes, max_rows, binom,
-                                           ctx->lut_hdr, ctx->lut, snp, sm)))
-          return fail(st, "packed pass launch failed");
-      } else {
-        const int64_t epb = gd_bounds_elems_per_block();
-        const unsigned gxb = (unsigned)std::min<int64_t>((mx + epb - 1) / epb, std::max(1, 8192 / nc));
-        hipLaunchKernelGGL(k_bounds, dim3(gxb, nc, 2), dim3(256), 0, sm, d_ch + c0, apos, bpos, wsize, wstep, lo_a,
-                           hi_a, lo_b, flags);
-        const unsigned gxs = (unsigned)std::min<int64_t>((amax + 255) / 256, std::max(1, 8192 / nc));
-        hipLaunchKernelGGL(k_snp_fet, dim3(gxs, nc), dim3(256), 0, sm, d_ch + c0, avals, bvals, binom,
-                           ctx->lut_hdr, ctx->lut, snp, fused ? 1 : 0);
-      }
-      HIP_TRY(hipGetLastError());
-      HIP_TRY(hipEventRecord(ctx->gev[g], sm));
-    }
-    HIP_TRY(hipEventRecord(ctx->ev[1], sm));
-    /* with G > 1 the groups' window kernels alternate between stream2 and the caller's stream,
-     * so two of them run at once (their outputs are disjoint, the declined-window list and the
-     * flags atomic); GD_WALT=0 keeps them all on stream2 (diagnostics) */
-    const char *walt = getenv("GD_WALT");
-    const bool alt = G > 1 && !(walt && walt[0] == '0');
-    for (int g = 0; g < G && !force_general; ++g) {
-      const int c0 = cuts[g], c1 = cuts[g + 1];
-      hipStream_t sw = (alt && (g & 1)) ? s : s2;
-      if (G > 1) HIP_TRY(hipStreamWaitEvent(sw, ctx->gev[g], 0));
-      st = gd_fet_window_fast_launch(d_ch, nchrom, d_blk, blk_off[c0], blk_off[c1] - blk_off[c0], lo_a, hi_a, lo_b,
-                                     snp, avals, bvals, binom, ctx->lut_hdr, ctx->lut, fused ? 1 : 0, perc, scores,
-                                     stddev, flags, list, list_count, sw);
-      if (st) return fail(st, "fast window kernel launch failed");
-    }
-    if (G > 1) {
-      /* ev[2] after every group's window kernel: the odd groups ran on s, the others on s2 */
-      HIP_TRY(hipEventRecord(ctx->ev[4], s2));
-      HIP_TRY(hipStreamWaitEvent(s, ctx->ev[4], 0));
-      HIP_TRY(hipStreamWaitEvent(s, ctx->ev[1], 0));
-    }
-    HIP_TRY(hipEventRecord(ctx->ev[2], s));
   }
+  if (fused) {
+    /* the per-SNP pass for chromosomes whose sizes the table does not hold (every workgroup
+     * exits at once otherwise): before any bounds pass, on a grid that costs nothing then */
+    int64_t amax = 1;
+    for (int c = 0; c < nchrom; ++c) amax = std::max<int64_t>(amax, pl.h[c].alen);
+    const unsigned gxs = (unsigned)std::min<int64_t>((amax + 255) / 256, std::max(1, 1024 / nchrom));
+    hipLaunchKernelGGL(k_snp_fet, dim3(gxs, nchrom), dim3(256), 0, sm, d_ch, avals, bvals, binom, ctx->lut_hdr,
+                       ctx->lut, snp, 1);
+  }
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipEventRecord(ctx->ev[1], sm)); /* end of the prologue */
+  std::vector<int> cuts(G + 1);
+  for (int g = 0; g <= G; ++g) cuts[g] = (int)((int64_t)nchrom * g / G);
+  auto bounds_pass = [&](int g) -> int {
+    const int c0 = cuts[g], nc = cuts[g + 1] - cuts[g];
+    int64_t amax = 1, mx = 1;
+    for (int c = c0; c < c0 + nc; ++c) {
+      amax = std::max<int64_t>(amax, pl.h[c].alen);
+      mx = std::max<int64_t>(mx, std::max(pl.h[c].alen, pl.h[c].blen) + 1);
+    }
+    if (pk) {
+      int r;
+      if ((r = gd_packed_bounds_launch(d_ch + c0, nc, d_roff + c0, pk->rowpos, max_rows, wsize, wstep, lo_a, hi_a,
+                                       lo_b, flags, sm)) ||
+          (r = gd_packed_snp_fet_launch(d_ch + c0, nc, d_woff + 2 * c0, pk->acodes, pk->bcodes, max_rows, binom,
+                                        ctx->lut_hdr, ctx->lut, snp, sm)))
+        return fail(r, "packed pass launch failed");
+    } else {
+      const int64_t epb = gd_bounds_elems_per_block();
+      const unsigned gxb = (unsigned)std::min<int64_t>((mx + epb - 1) / epb, std::max(1, 8192 / nc));
+      hipLaunchKernelGGL(k_bounds, dim3(gxb, nc, 2), dim3(256), 0, sm, d_ch + c0, apos, bpos, wsize, wstep, lo_a,
+                         hi_a, lo_b, flags);
+      if (!fused) {
+        const unsigned gxs = (unsigned)std::min<int64_t>((amax + 255) / 256, std::max(1, 8192 / nc));
+        hipLaunchKernelGGL(k_snp_fet, dim3(gxs, nc), dim3(256), 0, sm, d_ch + c0, avals, bvals, binom, ctx->lut_hdr,
+                           ctx->lut, snp, 0);
+      }
+    }
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(ctx->gev[g], sm));
+    return GD_OK;
+  };
+  auto window_pass = [&](int g) -> int {
+    const int c0 = cuts[g], c1 = cuts[g + 1];
+    hipStream_t sw = (g & 1) ? s : s2;
+    if (G > 1) HIP_TRY(hipStreamWaitEvent(sw, ctx->gev[g], 0));
+    const int r = gd_fet_window_fast_launch(d_ch, nchrom, d_blk, blk_off[c0], blk_off[c1] - blk_off[c0], lo_a, hi_a,
+                                            lo_b, snp, avals, bvals, binom, ctx->lut_hdr, ctx->lut, fused ? 1 : 0, perc,
+                                            scores, stddev, flags, list, list_count, sw);
+    return r ? fail(r, "fast window kernel launch failed") : GD_OK;
+  };
+  /* submission order bounds 0, bounds 1, windows 0, bounds 2, windows 1, ...: every window
+   * kernel is queued as soon as its bounds are, behind the next group's bounds pass */
+  for (int g = 0; g < G; ++g) {
+    if ((st = bounds_pass(g))) return st;
+    if (g > 0 && !force_general && (st = window_pass(g - 1))) return st;
+  }
+  if (!force_general && (st = window_pass(G - 1))) return st;
+  if (G > 1) {
+    /* ev[2] after every group's window kernel: the odd groups ran on s, the others on s2 */
+    HIP_TRY(hipEventRecord(ctx->ev[4], s2));
+    HIP_TRY(hipStreamWaitEvent(s, ctx->ev[4], 0));
+    HIP_TRY(hipStreamWaitEvent(s, ctx->gev[G - 1], 0));
+  }
+  HIP_TRY(hipEventRecord(ctx->ev[2], s));
   {
     /* windows the fast path declined: literal one-workgroup-per-window path */
     const unsigned gx = (unsigned)std::min<int64_t>(pl.wtotal, 4096);

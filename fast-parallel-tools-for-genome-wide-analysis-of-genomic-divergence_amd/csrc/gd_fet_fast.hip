@@ -35,7 +35,6 @@
 #include <cstring>
 
 #include "../../include/gdscan.h"
-#include "gd_bounds.h"
 #include "gd_common.h"
 #include "gd_fet_rows.h"
 #include "gd_internal.h"
@@ -614,99 +613,6 @@ __device__ __forceinline__ void fw_clean8(double (&v)[8]) {
 #undef FW_CX2
 }
 
-/* Bounds tiles of a scheduled scan: tile t covers FW_BT_ELEMS positions of one population
- * of one chromosome, the tiles chromosome-major (A, then B), bt_off[c] = first tile of
- * chromosome c (host: gd_fet_bounds_tiles).  A tile is 4 waves x FW_BT_SEGS segments of
- * 256 FW_BT_CH elements (gd_bounds.h); bdone[c] counts a chromosome's tiles once every
- * lane's device-scope stores of them have completed; window workgroups read the ranges
- * back at device scope (gd_bounds.h). */
-#define FW_BT_CH GD_FET_BT_CH
-#define FW_BT_SEGS GD_FET_BT_SEGS
-#define FW_BT_ELEMS GD_FET_BT_ELEMS
-static_assert(4 * 256 * FW_BT_CH * 4 <= FW_SPAN * 8, "the bounds workers' LDS slices live in sh_span");
-
-#ifdef GD_FET_WPROF
-/* diagnostics build only: cycles of the scheduled scan's phases summed over workgroups
- * (thread 0): [0] tile lookup, [1] loads + walk, [2] store drain + count, [3] tiles,
- * [4] window workgroups' waits, [5] window workgroups */
-__device__ unsigned long long g_fw_wprof[8];
-#define FW_WP(i, v) atomicAdd(&g_fw_wprof[i], (unsigned long long)(v))
-#else
-#define FW_WP(i, v)
-#endif
-
-__device__ void fw_bounds_worker(int t0, const gd_fet_sched &sc, const gd_chrom_dev *ch, int nchrom, int32_t *lo_a,
-                                 int32_t *hi_a, int32_t *lo_b, unsigned *flags, int32_t *lds) {
-  const int total = sc.bt_off[nchrom];
-  const int wave = threadIdx.x >> 6;
-  int32_t *sg = lds + wave * 256 * FW_BT_CH;
-  /* the SIMDs' other waves are VALU-bound window workgroups: the workers' few instructions
-   * issue first, so the bounds keep ahead of the windows that wait for them */
-  __builtin_amdgcn_s_setprio(3);
-#ifdef GD_FET_WPROF
-  uint64_t tp = __builtin_readcyclecounter();
-#define FW_WT(i)                                            \
-  do {                                                      \
-    const uint64_t t_ = __builtin_readcyclecounter();       \
-    if (threadIdx.x == 0) FW_WP(i, t_ - tp);                \
-    tp = t_;                                                \
-  } while (0)
-#else
-#define FW_WT(i)
-#endif
-  /* the worker's tiles t0, t0 + nb, ... ascend, so its chromosome only moves forward; it
-   * counts its tiles of the current chromosome and publishes them when it moves on: one
-   * store drain per chromosome, not per tile */
-  int c = 0, mine = 0, jc = -1, jpop = -1, ta = 0;
-  int32_t c_beg = sc.bt_off[0], c_end = sc.bt_off[1];
-  gd_bounds_job job; /* of (jc, jpop), rebuilt when the tile's population changes */
-  unsigned uns = 0;
-  auto publish = [&]() {
-    if (uns) atomicOr(flags, uns);
-    uns = 0;
-    /* the tiles' device-scope stores have completed before they are counted (no L2
-     * write-back: they were written through) */
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0 && mine > 0)
-      __hip_atomic_fetch_add(&sc.bdone[c * sc.bstride], (unsigned)mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    mine = 0;
-  };
-  for (int t = t0; t < total; t += sc.nb) {
-    if (t >= c_end) {
-      publish();
-      do {
-        ++c;
-        c_beg = c_end;
-        c_end = sc.bt_off[c + 1];
-      } while (t >= c_end); /* empty chromosomes own no tile */
-    }
-    if (c != jc) ta = (int)(((int64_t)ch[c].alen + FW_BT_ELEMS) / FW_BT_ELEMS); /* gd_fet_bounds_tiles(alen) */
-    int local = t - c_beg;
-    const int pop = local >= ta;
-    if (pop) local -= ta;
-    if (c != jc || pop != jpop) {
-      job.init(ch[c], pop, sc.apos, sc.bpos, sc.wsize, sc.wstep, lo_a, hi_a, lo_b);
-      jc = c;
-      jpop = pop;
-    }
-    FW_WT(0);
-    bool dec = false;
-#pragma unroll
-    for (int k = 0; k < FW_BT_SEGS; ++k) {
-      const int64_t seg = (int64_t)local * FW_BT_ELEMS + (int64_t)(4 * k + wave) * (256 * FW_BT_CH);
-      if (seg <= job.len) dec |= job.segment<FW_BT_CH, true>(seg, sg);
-    }
-    if (dec) uns |= pop ? GD_FLAG_UNSORTED_B : GD_FLAG_UNSORTED_A;
-    ++mine;
-    FW_WT(1);
-    if (threadIdx.x == 0) FW_WP(3, 1);
-  }
-  publish();
-  FW_WT(2);
-#undef FW_WT
-}
-
 /* register-allocation target: 7 waves per SIMD (the LDS limit of 7 workgroups per CU); left
  * to itself the allocator takes 76 VGPRs (6 waves) for the FW_LCG_MAD step, and 7 waves ran
  * 0.7-1 % faster (C2: 2.365-2.380 against 2.383-2.385 ms/step; FW_LCG_MAD=0: 2.397-2.412) */
@@ -716,10 +622,10 @@ __device__ void fw_bounds_worker(int t0, const gd_fet_sched &sc, const gd_chrom_
 #define FW_WPE __attribute__((amdgpu_waves_per_eu(FW_WAVES_PER_SIMD, 8)))
 __global__ void __launch_bounds__(FW_WPB *FW_TPW) FW_WPE
     k_fet_window_fast(const gd_chrom_dev *ch, int nchrom, const int32_t *blk_off, int blk_base,
-                      int32_t *lo_a, int32_t *hi_a, int32_t *lo_b, const double *snp_score,
+                      const int32_t *lo_a, const int32_t *hi_a, const int32_t *lo_b, const double *snp_score,
                       const double *avals, const double *bvals, const uint64_t *binom, const int *lut_hdr,
                       const double *lut, int fused, double perc, double *scores, double *stddev,
-                      unsigned *flags, int32_t *slow_list, unsigned *slow_count, const gd_fet_sched *scp) {
+                      const unsigned *flags, int32_t *slow_list, unsigned *slow_count) {
   __shared__ double sh_span[FW_SPAN];
   /* the row counters of the span staging (fused mode) share LDS with the ranked top
    * scores and the replicate rank pairs, which are written only after it */
@@ -738,24 +644,10 @@ __global__ void __launch_bounds__(FW_WPB *FW_TPW) FW_WPE
   __shared__ int sh_rej[FW_WPB][FW_MAXREJ];
   __shared__ unsigned long long sh_lo, sh_hi;
 
+  if (*flags & (GD_FLAG_UNSORTED_A | GD_FLAG_UNSORTED_B | GD_FLAG_BAD_SIZE)) return;
+  FW_PROF_INIT;
   const int tid = threadIdx.x;
-  int b = blk_base + blockIdx.x;
-  if (scp) {
-    const gd_fet_sched &sc = *scp;
-    /* scheduled scan: workgroups take tickets in the order they start; the first sc.nb
-     * tickets run the bounds pass (fw_bounds_worker) and never wait, every later one is a
-     * window workgroup, which waits until its chromosome's bounds tiles are done -- tiles
-     * held by workgroups that started before it, so the wait always ends */
-    __shared__ int sh_ticket;
-    if (tid == 0) sh_ticket = (int)atomicAdd(sc.ticket, 1u);
-    __syncthreads();
-    const int t = sh_ticket;
-    if (t < sc.nb) {
-      fw_bounds_worker(t, sc, ch, nchrom, lo_a, hi_a, lo_b, flags, reinterpret_cast<int32_t *>(sh_span));
-      return;
-    }
-    b = t - sc.nb;
-  }
+  const int b = blk_base + blockIdx.x;
   /* workgroups never straddle chromosomes: blk_off[c] = first workgroup of chromosome c */
   int cb = 0;
   {
@@ -769,26 +661,6 @@ __global__ void __launch_bounds__(FW_WPB *FW_TPW) FW_WPE
     }
     cb = lo;
   }
-  if (scp) {
-    const gd_fet_sched &sc = *scp;
-    if (tid == 0) {
-#ifdef GD_FET_WPROF
-      const uint64_t tw = __builtin_readcyclecounter();
-#endif
-      const unsigned need = (unsigned)(sc.bt_off[cb + 1] - sc.bt_off[cb]);
-      while (__hip_atomic_load(&sc.bdone[cb * sc.bstride], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need)
-        for (int k = 0; k < sc.poll; ++k) __builtin_amdgcn_s_sleep(16);
-#ifdef GD_FET_WPROF
-      FW_WP(4, __builtin_readcyclecounter() - tw);
-      FW_WP(5, 1);
-#endif
-    }
-    __syncthreads();
-  }
-  if (__hip_atomic_load(flags, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) &
-      (GD_FLAG_UNSORTED_A | GD_FLAG_UNSORTED_B | GD_FLAG_BAD_SIZE))
-    return;
-  FW_PROF_INIT;
   const gd_chrom_dev &d = ch[cb];
   const int64_t g0 = d.w_base + (int64_t)(b - blk_off[cb]) * FW_WPB;
   const int64_t wtotal = d.w_base + d.wend; /* end of this chromosome's windows */
@@ -804,10 +676,7 @@ __global__ void __launch_bounds__(FW_WPB *FW_TPW) FW_WPE
     int64_t row = -1;
     int n = 0;
     if (g < wtotal) {
-      /* scheduled: written in this kernel, read at device scope past this XCD's L2 */
-      const int lo = scp ? __hip_atomic_load(lo_a + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : lo_a[g];
-      const int hi = scp ? __hip_atomic_load(hi_a + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : hi_a[g];
-      const int lb = scp ? __hip_atomic_load(lo_b + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : lo_b[g];
+      const int lo = lo_a[g], hi = hi_a[g], lb = lo_b[g];
       n = (hi - lo) / d.asize;
       const bool aligned = n > 0 && (lo % d.asize == 0) && (lb % d.bsize == 0) && (lo / d.asize == lb / d.bsize) &&
                            (lo / d.asize + n <= d.nrows);
@@ -1142,8 +1011,6 @@ __global__ void __launch_bounds__(FW_WPB *FW_TPW) FW_WPE
   FW_PROF(4);
 }
 
-__global__ void k_zero_count(unsigned *count) { *count = 0; }
-
 /* GD_FORCE_GENERAL=1: every window takes the literal path (self-consistency checks) */
 __global__ void k_all_windows(int32_t *list, unsigned *count, int64_t wtotal) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1159,8 +1026,8 @@ int gd_fet_fast_init(hipStream_t s) {
   return hipGetLastError() == hipSuccess ? GD_OK : GD_ERR_HIP;
 }
 
-/* Resets the slow-path list; with GD_FORCE_GENERAL=1 fills it with every window and
- * tells the caller to skip the fast kernels. */
+/* GD_FORCE_GENERAL=1: fills the slow-path list (zeroed with the scan's flags) with every
+ * window and tells the caller to skip the fast kernels. */
 int gd_fet_window_prepare(int64_t wtotal, int32_t *slow_list, unsigned *slow_count, hipStream_t s,
                           bool *force_general) {
   const char *force = getenv("GD_FORCE_GENERAL");
@@ -1168,10 +1035,9 @@ int gd_fet_window_prepare(int64_t wtotal, int32_t *slow_list, unsigned *slow_cou
   if (*force_general)
     hipLaunchKernelGGL(k_all_windows, dim3((unsigned)((wtotal + 255) / 256)), dim3(256), 0, s, slow_list,
                        slow_count, wtotal);
-  else
-    hipLaunchKernelGGL(k_zero_count, dim3(1), dim3(1), 0, s, slow_count);
   return hipGetLastError() == hipSuccess ? GD_OK : GD_ERR_HIP;
 }
+
 
 /* workgroups [blk_begin, blk_begin + blk_count) of the chromosome-aligned grid */
 /* fused: the span scores come from avals/bvals and the score table (snp_score is then
@@ -1193,37 +1059,9 @@ int gd_fet_window_fast_launch(const gd_chrom_dev *ch, int nchrom, const int32_t 
       fprintf(stderr, "fet-prof cycles: A1 %llu A2 %llu B %llu Bp %llu C %llu\n", h[0], h[1], h[2], h[3], h[4]);
   }
 #endif
-  hipLaunchKernelGGL(k_fet_window_fast, dim3((unsigned)blk_count), dim3(FW_WPB * FW_TPW), 0, s, ch, nchrom, blk_off,
-                     blk_begin, const_cast<int32_t *>(lo_a), const_cast<int32_t *>(hi_a), const_cast<int32_t *>(lo_b),
-                     snp_score, avals, bvals, binom, lut_hdr, lut, fused, perc, scores, stddev, flags, slow_list,
-                     slow_count, (const gd_fet_sched *)nullptr);
+  hipLaunchKernelGGL(k_fet_window_fast, dim3((unsigned)blk_count), dim3(FW_WPB * FW_TPW), 0, s, ch, nchrom,
+                     blk_off, blk_begin, lo_a, hi_a, lo_b, snp_score, avals, bvals, binom, lut_hdr, lut, fused, perc,
+                     scores, stddev, flags, slow_list, slow_count);
   return hipGetLastError() == hipSuccess ? GD_OK : GD_ERR_HIP;
 }
 
-/* the scheduled fused scan (gd_api.hip): sc.nb bounds workers + blk_count window workgroups,
- * ordered by ticket; d_sc in device memory, its ticket and bdone zeroed, bt_off from gd_fet_bounds_tiles) */
-int gd_fet_window_sched_launch(const gd_chrom_dev *ch, int nchrom, const int32_t *blk_off, int blk_count,
-                               int32_t *lo_a, int32_t *hi_a, int32_t *lo_b, const double *snp_score,
-                               const double *avals, const double *bvals, const uint64_t *binom, const int *lut_hdr,
-                               const double *lut, double perc, double *scores, double *stddev, unsigned *flags,
-                               int32_t *slow_list, unsigned *slow_count, const gd_fet_sched *d_sc, int nb,
-                               hipStream_t s) {
-  if (blk_count <= 0 && nb <= 0) return GD_OK;
-#ifdef GD_FET_WPROF
-  {
-    static int calls = 0;
-    unsigned long long h[8];
-    (void)hipStreamSynchronize(s);
-    (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(g_fw_wprof), sizeof h);
-    if (++calls % 8 == 0 && h[3] > 0 && h[5] > 0)
-      fprintf(stderr, "fet-wprof per tile: setup %.0f walk %.0f drain %.0f cycles (%llu tiles); wait %.0f cycles per window workgroup (%llu)\n",
-              (double)h[0] / h[3], (double)h[1] / h[3], (double)h[2] / h[3], h[3], (double)h[4] / h[5], h[5]);
-    memset(h, 0, sizeof h);
-    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_fw_wprof), h, sizeof h);
-  }
-#endif
-  hipLaunchKernelGGL(k_fet_window_fast, dim3((unsigned)(blk_count + nb)), dim3(FW_WPB * FW_TPW), 0, s, ch, nchrom,
-                     blk_off, 0, lo_a, hi_a, lo_b, snp_score, avals, bvals, binom, lut_hdr, lut, 1, perc, scores,
-                     stddev, flags, slow_list, slow_count, d_sc);
-  return hipGetLastError() == hipSuccess ? GD_OK : GD_ERR_HIP;
-}

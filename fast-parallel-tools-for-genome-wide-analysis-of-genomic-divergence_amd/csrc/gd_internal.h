@@ -25,26 +25,6 @@ typedef struct gd_chrom_dev {
   uint64_t seed;
 } gd_chrom_dev;
 
-/* Scheduled FET scan (gd_fet_fast.hip, gd_api.hip): the window kernel's workgroups take
- * tickets; the first nb run the bounds pass in tiles of GD_FET_BT_ELEMS positions (one
- * population of one chromosome; bt_off[c] = first tile of chromosome c, A's tiles then
- * B's), the rest are window workgroups that wait for bdone[c] == their chromosome's tiles. */
-#define GD_FET_BT_CH 2   /* int4 loads per lane per segment of 256 GD_FET_BT_CH positions */
-#define GD_FET_BT_SEGS 1 /* segments per wave per tile (4 waves), their loads in flight together */
-#define GD_FET_BT_ELEMS (4 * GD_FET_BT_SEGS * 256 * GD_FET_BT_CH)
-/* tiles of one population's positions: segments start at 0 .. len (len = the sentinel) */
-static inline int gd_fet_bounds_tiles(int64_t len) { return (int)((len + GD_FET_BT_ELEMS) / GD_FET_BT_ELEMS); }
-typedef struct gd_fet_sched {
-  unsigned *ticket; /* NULL: an unscheduled launch (window workgroup = blockIdx) */
-  unsigned *bdone;  /* per chromosome: bounds tiles written */
-  const int32_t *bt_off;
-  const int32_t *apos, *bpos;
-  int nb; /* bounds-worker workgroups */
-  int wsize, wstep;
-  int bstride; /* words between two chromosomes' bdone counters */
-  int poll;    /* s_sleep 16 rounds between two polls of a waiting window workgroup */
-} gd_fet_sched;
-
 /* status bits raised by kernels into one device word */
 #define GD_FLAG_UNSORTED_A 1u
 #define GD_FLAG_UNSORTED_B 2u
@@ -53,10 +33,7 @@ typedef struct gd_fet_sched {
 
 /* general-path window capacity held in LDS; larger windows use global scratch */
 #define GD_GEN_LDS_N 1024
-#define GD_MAX_GROUPS 32    /* chromosome groups pipelined across two streams (capacity) */
-#define GD_DEFAULT_GROUPS 2 /* groups used by default, their window kernels on alternating streams (r04: 2.288-2.317
-                               against 2.312-2.339 ms per C2 scan with one group; r03, without the alternation, 2 groups
-                               were slower: 2.64 against 2.58) */
+#define GD_MAX_GROUPS 32 /* chromosome groups pipelined across the scan's streams (capacity) */
 #define GD_LUT_CAP (1 << 22) /* FET score-table entries (32 MB): up to ~62+62 individuals */
 #define GD_NREP 100 /* bootstrap replicates (cFisher.c:62) */
 
