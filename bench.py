@@ -386,21 +386,93 @@ def host_run(args, lib, _lib, check, avals, bvals, apos, bpos, chroms, nch, scor
     pd_ = lambda x: x.ctypes.data_as(C.POINTER(C.c_double))
     pi_ = lambda x: x.ctypes.data_as(C.POINTER(C.c_int))
     pv_ = lambda x: x.ctypes.data
-    t_ref, s1, d1 = timed(lambda s_, d_: check(lib.gd_fet_scan_host_batch(
+    ref_call = lambda s_, d_: check(lib.gd_fet_scan_host_batch(
         hc, nh, pd_(av), pd_(bv), pi_(ap), pi_(bp), args.wsize, args.wstep, args.perc, _lib.GD_WINDOWS_THREADED,
-        pd_(s_), pd_(d_))))
+        pd_(s_), pd_(d_)))
+    t_ref, s1, d1 = timed(ref_call)  # packed on host threads inside the call (gd_api.hip host_packed)
+    os.environ["GD_HOST_NOPACK"] = "1"
+    try:
+        t_raw, s3, d3 = timed(ref_call)  # the reference layout across PCIe (12 B per genotype)
+    finally:
+        os.environ.pop("GD_HOST_NOPACK", None)
     t_pk, s2, d2 = timed(lambda s_, d_: check(lib.gd_fet_scan_packed_host(
         pcs, nh, pv_(hac), pv_(hbc), pv_(hrp), args.wsize, args.wstep, args.perc, lib.gd_get_fet_mode(),
         _lib.GD_WINDOWS_THREADED, pd_(s_), pd_(d_))))
     ref_bytes = 12 * (na + nb) + 16 * nw
     pk_bytes = 8 * nh * nsnp * (wa + wb) + 4 * nh * nsnp + 16 * nw
+    usable, _, _ = host_cpus()
     return {"sample": f"{nh} x {nsnp} SNPs, {windows} windows, host buffers, best of 3",
             "reference_layout": {"ms": t_ref * 1e3, "windows_per_s": windows / t_ref,
-                                 "host_bytes": ref_bytes, "GB_per_s": ref_bytes / t_ref / 1e9},
+                                 "host_bytes": ref_bytes, "GB_per_s": ref_bytes / t_ref / 1e9,
+                                 "how": f"packed on {min(usable, 16)} host threads inside the call, 2 bits per "
+                                        "genotype + 4 B per row across PCIe"},
+            "reference_layout_unpacked": {"ms": t_raw * 1e3, "windows_per_s": windows / t_raw,
+                                          "GB_per_s": ref_bytes / t_raw / 1e9, "how": "GD_HOST_NOPACK=1"},
             "packed": {"ms": t_pk * 1e3, "windows_per_s": windows / t_pk,
                        "host_bytes": pk_bytes, "GB_per_s": pk_bytes / t_pk / 1e9},
             "parity": bool(np.array_equal(s1, ref_s) and np.array_equal(d1, ref_d)
-                           and np.array_equal(s2, ref_s) and np.array_equal(d2, ref_d))}
+                           and np.array_equal(s2, ref_s) and np.array_equal(d2, ref_d)
+                           and np.array_equal(s3, ref_s) and np.array_equal(d3, ref_d))}
+
+
+def c1_run(args):
+    """configs[0] (FET, one synthetic chromosome: 50k SNPs, 10+10, 2.5 kb windows; the
+    reference's Pthreads CPU path): the reference's own threadcompute (oracle/_ref, 64
+    pthreads) and the drop-in call HyperBrowser makes, gdscan.fet.fisher_exact_tester
+    (FisherExactScoreStat.py:51-58 -> fisher_cython_parallel.pyx:14-15), on the same host
+    arrays -- per call: host packing, PCIe both ways, the scan -- plus one C2-sized chromosome
+    (500k SNPs, 20+20) through the same call.  Scores compared bit for bit (seed-independent;
+    the reference's stddev is time-seeded)."""
+    from gdscan import fet, synth
+    ref = ROOT / "oracle" / "_ref" / "libref_fisher.so"
+    DP = np.ctypeslib.ndpointer(np.float64, flags="C")
+    IP = np.ctypeslib.ndpointer(np.int32, flags="C")
+    rfn = None
+    if ref.exists():
+        rl = ctypes.CDLL(str(ref))
+        rfn = rl.threadcompute
+        rfn.argtypes = [DP, DP, IP, IP] + [ctypes.c_int] * 6 + [ctypes.c_double, DP, DP]
+    out = {}
+    for key, (chrom, nsnp, a, b) in (("c1_50k_10x10", (0, 50_000, 10, 10)), ("chrom_500k_20x20", (1, 500_000, 20, 20))):
+        av, bv, ap, bp, regend = synth.chromosome(chrom, nsnp, a, b)
+        n = regend // args.wstep
+        win = fet.window_count(regend, args.wsize, args.wstep)
+
+        def best(fn, reps):
+            t = None
+            for _ in range(reps):
+                s_, d_ = np.zeros(n), np.zeros(n)
+                t0 = time.perf_counter()
+                fn(s_, d_)
+                dt = time.perf_counter() - t0
+                t = dt if t is None or dt < t else t
+            return t, s_, d_
+
+        drop = lambda s_, d_: fet.fisher_exact_tester(av, bv, ap, bp, 0, regend, args.wsize, args.wstep, len(av),
+                                                      len(bv), args.perc, s_, d_)
+        best(drop, 1)  # context, pinned buffers
+        t_gpu, sg, dg = best(drop, 5)
+        os.environ["GD_HOST_NOPACK"] = "1"
+        try:
+            t_raw, _, _ = best(drop, 3)
+        finally:
+            os.environ.pop("GD_HOST_NOPACK", None)
+        o = {"snps": nsnp, "individuals": f"{a}+{b}", "windows": win,
+             "dropin": {"ms": t_gpu * 1e3, "windows_per_s": win / t_gpu,
+                        "call": "gdscan.fet.fisher_exact_tester (host arrays in and out, packed on host threads)"},
+             "dropin_unpacked": {"ms": t_raw * 1e3, "windows_per_s": win / t_raw, "how": "GD_HOST_NOPACK=1"}}
+        if rfn is not None:
+            t_ref, sr, _ = best(lambda s_, d_: silenced(lambda: rfn(av, bv, ap, bp, 0, regend, args.wsize, args.wstep,
+                                                                    len(av), len(bv), args.perc, s_, d_)), 2)
+            comp = (sr != 0) | (sg != 0)
+            o["reference"] = {"ms": t_ref * 1e3, "windows_per_s": win / t_ref, "kind": "reference",
+                              "call": "threadcompute (oracle/_ref, built from the reference sources), 64 pthreads",
+                              "cores": min(64, host_cpus()[0])}
+            o["parity_windows"] = int(comp.sum())
+            o["parity_bit_exact"] = bool(np.array_equal(sr[comp], sg[comp]))
+            o["speedup_vs_reference"] = t_ref / t_gpu
+        out[key] = o
+    return out
 
 
 # ----------------------------------------------------------------------------- CSS legs
@@ -1005,6 +1077,9 @@ def main():
         if rank == 0 and world == 1:
             out["host_path"] = host_run(args, lib, _lib, check, avals, bvals, apos, bpos, chroms, nch, scores, stddev,
                                         codes)
+        if rank == 0 and not args.no_cpu:
+            note(rank, "C1 (configs[0]) and the per-chromosome drop-in call")
+            out["c1"] = c1_run(args)
         del codes
 
     if not args.no_css:

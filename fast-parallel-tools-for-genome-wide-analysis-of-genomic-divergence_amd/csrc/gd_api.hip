@@ -17,6 +17,7 @@
 #include <cmath>
 #include <cstring>
 #include <mutex>
+#include <type_traits>
 #include <string>
 #include <vector>
 
@@ -75,18 +76,18 @@ int gd_css_launch(int mp, int drosophila, int mds, const gd_chrom_dev *d_ch, int
 int gd_synth_launch(int chrom, int nsnp, int asize, int bsize, uint64_t seed, const double *freq_table,
                     double *avals, double *bvals, int32_t *apos, int32_t *bpos, hipStream_t s);
 
-/* general-path grid (gd_internal.h): resident capacity of the current device */
+/* general-path grid (gd_internal.h): resident capacity of the current device (CU counts
+ * cached per device: a process may drive devices of different sizes) */
 int64_t gd_css_big_grid(int64_t wtotal, int mp) {
-  static std::atomic<int> cus{0};
-  int n = cus.load();
+  constexpr int NDEV = 64;
+  static std::atomic<int> cus[NDEV];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0) dev = 0;
+  int n = dev < NDEV ? cus[dev].load() : 0;
   if (n == 0) {
-    int dev = 0, v = 0;
-    if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) ==
-                                                 hipSuccess && v > 0)
-      n = v;
-    else
-      n = 256;
-    cus.store(n);
+    int v = 0;
+    n = (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0) ? v : 256;
+    if (dev < NDEV) cus[dev].store(n);
   }
   int64_t grid = (int64_t)n * (mp <= 256 ? 4 : 2);
   if (const char *e = getenv("GD_CSS_BIG_GRID")) {
@@ -98,6 +99,7 @@ int64_t gd_css_big_grid(int64_t wtotal, int mp) {
 
 /* ------------------------------------------------------------------ errors */
 static thread_local std::string g_err;
+static thread_local int g_status = GD_OK; /* the status that went with g_err (gd_last_status) */
 /* seed of the reference-signature entry points: per calling thread (gd_set_seed affects
  * only the thread that calls it; every thread starts at GD_DEFAULT_SEED), so two threads
  * that each set a seed and call fisher_exact_tester cannot race on it */
@@ -107,9 +109,18 @@ static thread_local float g_stage_ms[GD_NSTAGES];
 
 static int fail(int code, const std::string &msg) {
   g_err = msg;
+  g_status = code;
   return code;
 }
-void gd_set_error(const char *msg) { g_err = msg ? msg : ""; } /* for gd_gtrack.cpp */
+/* for gd_gtrack.cpp / gd_pack.cpp */
+void gd_set_error(const char *msg) {
+  g_err = msg ? msg : "";
+  g_status = GD_ERR_ARG;
+}
+void gd_set_status_error(int code, const char *msg) {
+  g_err = msg ? msg : "";
+  g_status = code;
+}
 
 #define HIP_TRY(expr)                                                                     \
   do {                                                                                    \
@@ -144,6 +155,8 @@ struct gd_ctx {
   hipEvent_t stage_ev = nullptr; /* after the last copy out of h_stage (recorded by h2d) */
   bool stage_live = false;       /* stage_ev was recorded since the buffer was last reset */
   unsigned *h_flags_dev = nullptr; /* one device word (packer status) */
+  char *h_pack = nullptr;          /* pinned: host-packed tracks of the reference-signature calls */
+  size_t h_pack_cap = 0;
 };
 
 static int ctx_init(gd_ctx *c, int device) {
@@ -224,6 +237,7 @@ extern "C" void gd_ctx_destroy(gd_ctx *c) {
   if (c->stream_mem) (void)hipStreamDestroy(c->stream_mem);
   if (c->h_flags) (void)hipHostFree(c->h_flags);
   if (c->h_stage) (void)hipHostFree(c->h_stage);
+  if (c->h_pack) (void)hipHostFree(c->h_pack);
   if (c->h_flags_dev) (void)hipFree(c->h_flags_dev);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
@@ -654,10 +668,124 @@ extern "C" int gd_fet_scan_device(gd_ctx *ctx, const gd_chrom *chroms, int nchro
                                g_fet_mode.load(), window_set, scores, stddev, hip_stream);
 }
 
-/* one chromosome from host memory: H2D, device scan, D2H of the outputs */
+extern "C" int gd_pack_rows_mt(const double *avals, const double *bvals, const int *apos, const int *bpos, int asize,
+                               int bsize, int64_t r0, int64_t r1, uint64_t *acodes, uint64_t *bcodes, int32_t *rowpos);
+
+/* The reference-signature host entry points over packed tracks.  When every chromosome's
+ * host arrays are whole rows of the four genotype codes with one position per row
+ * (gd_pack_shape and gd_pack_chrom_mt accept them -- the tracks VCFConvert writes), they are
+ * packed on host threads into the context's pinned buffer, and 2 bits per genotype plus 4 B
+ * per row cross PCIe instead of 12 B per genotype; the packed scan equals the reference-
+ * layout scan of the same tracks (tests/test_packed.py, test_host_pack_gpu.py).  Returns
+ * GD_HOST_NOPACK (nothing done) when a chromosome has no packed form: the caller then ships
+ * the reference layout.  GD_HOST_NOPACK=1 in the environment disables the route. */
+static constexpr int GD_HOST_NOPACK = 1;
+
 template <class Run>
+static int host_packed(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, const double *avals, const double *bvals,
+                       const int *apos, const int *bpos, int wstep, double *out0, double *out1, Run run) {
+  if (const char *e = getenv("GD_HOST_NOPACK"))
+    if (e[0] == '1') return GD_HOST_NOPACK;
+  std::vector<gd_pchrom> pc(nchrom);
+  int64_t rows = 0, wa_tot = 0, wb_tot = 0, nw = 0;
+  for (int c = 0; c < nchrom; ++c) {
+    const gd_chrom &h = chroms[c];
+    int asz = 0, bsz = 0, nr = 0;
+    if (h.alen > 0 && h.blen > 0) {
+      const std::string saved = g_err; /* a refusal here is not the call's error */
+      const int saved_st = g_status;
+      if (gd_pack_shape(apos + h.a_off, bpos + h.b_off, h.alen, h.blen, &asz, &bsz, &nr) != GD_OK) {
+        g_err = saved;
+        g_status = saved_st;
+        return GD_HOST_NOPACK;
+      }
+    }
+    gd_pchrom &q = pc[c];
+    std::memset(&q, 0, sizeof q);
+    q.row_off = rows;
+    q.a_word = wa_tot;
+    q.b_word = wb_tot;
+    q.nrows = nr;
+    q.asize = asz > 0 ? asz : 1;
+    q.bsize = bsz > 0 ? bsz : 1;
+    q.regend = h.regend;
+    q.w_out = h.w_out;
+    q.seed = h.seed;
+    rows += nr;
+    wa_tot += (int64_t)nr * GD_PACK_WORDS(q.asize);
+    wb_tot += (int64_t)nr * GD_PACK_WORDS(q.bsize);
+    nw = std::max<int64_t>(nw, h.w_out + std::max(h.regend, 0) / wstep);
+  }
+  if (nw == 0) return GD_OK;
+  /* pinned layout: A codes, B codes, row positions */
+  const size_t ba = sizeof(uint64_t) * std::max<int64_t>(wa_tot, 1), bb = sizeof(uint64_t) * std::max<int64_t>(wb_tot, 1);
+  const size_t br = sizeof(int32_t) * std::max<int64_t>(rows, 1), need = ba + bb + br + 512;
+  if (need > ctx->h_pack_cap) {
+    HIP_TRY(hipStreamSynchronize(ctx->stream)); /* no copy out of the old buffer is in flight */
+    if (ctx->h_pack) (void)hipHostFree(ctx->h_pack);
+    ctx->h_pack = nullptr;
+    ctx->h_pack_cap = 0;
+    const size_t cap = need + need / 4;
+    HIP_TRY(hipHostMalloc(&ctx->h_pack, cap));
+    ctx->h_pack_cap = cap;
+  }
+  uint64_t *hac = reinterpret_cast<uint64_t *>(ctx->h_pack), *hbc = hac + ba / 8;
+  int32_t *hrp = reinterpret_cast<int32_t *>(hbc + bb / 8);
+  int st;
+  const size_t dneed = ba + bb + br + 2 * sizeof(double) * nw + 1024;
+  if ((st = grow(&ctx->io, &ctx->io_cap, dneed))) return st;
+  Carve k{ctx->io};
+  uint64_t *ca = k.take<uint64_t>(ba / 8), *cb = k.take<uint64_t>(bb / 8);
+  int32_t *rp = k.take<int32_t>(br / 4);
+  double *o0 = k.take<double>(nw), *o1 = k.take<double>(nw);
+  hipStream_t s = ctx->stream;
+  HIP_TRY(hipMemcpyAsync(o0, out0, sizeof(double) * nw, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(o1, out1, sizeof(double) * nw, hipMemcpyHostToDevice, s));
+  /* chunks of ~8M genotypes: chunk j's codes cross PCIe (DMA from pinned memory) while the
+   * host threads pack chunk j + 1 */
+  for (int c = 0; c < nchrom; ++c) {
+    const gd_chrom &h = chroms[c];
+    const gd_pchrom &q = pc[c];
+    if (q.nrows == 0) continue;
+    const int wa = GD_PACK_WORDS(q.asize), wb = GD_PACK_WORDS(q.bsize);
+    const int64_t chunk = std::max<int64_t>(1, ((int64_t)8 << 20) / (q.asize + q.bsize));
+    for (int64_t r0 = 0; r0 < q.nrows; r0 += chunk) {
+      const int64_t r1 = std::min<int64_t>(q.nrows, r0 + chunk);
+      const std::string saved = g_err;
+      const int saved_st = g_status;
+      if (gd_pack_rows_mt(avals + h.a_off, bvals + h.b_off, apos + h.a_off, bpos + h.b_off, q.asize, q.bsize, r0, r1,
+                          hac + q.a_word, hbc + q.b_word, hrp + q.row_off) != GD_OK) {
+        g_err = saved;
+        g_status = saved_st;
+        HIP_TRY(hipStreamSynchronize(s)); /* the chunks already on their way read the pinned buffer */
+        return GD_HOST_NOPACK;
+      }
+      HIP_TRY(hipMemcpyAsync(ca + q.a_word + r0 * wa, hac + q.a_word + r0 * wa, sizeof(uint64_t) * (r1 - r0) * wa,
+                             hipMemcpyHostToDevice, s));
+      HIP_TRY(hipMemcpyAsync(cb + q.b_word + r0 * wb, hbc + q.b_word + r0 * wb, sizeof(uint64_t) * (r1 - r0) * wb,
+                             hipMemcpyHostToDevice, s));
+      HIP_TRY(hipMemcpyAsync(rp + q.row_off + r0, hrp + q.row_off + r0, sizeof(int32_t) * (r1 - r0),
+                             hipMemcpyHostToDevice, s));
+    }
+  }
+  const PackedIn pk{pc.data(), ca, cb, rp};
+  if ((st = run(ctx, pk, nchrom, o0, o1, s))) {
+    (void)hipStreamSynchronize(s); /* the pinned buffer may still be read */
+    return st;
+  }
+  HIP_TRY(hipMemcpyAsync(out0, o0, sizeof(double) * nw, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(out1, o1, sizeof(double) * nw, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  return GD_OK;
+}
+
+/* one chromosome from host memory: H2D, device scan, D2H of the outputs; packed when the
+ * tracks allow it and the call passes a packed runner (host_packed) */
+struct NoPack {};
+template <class Run, class RunP = NoPack>
 static int host_scan(const double *avals, const double *bvals, const int *apos, const int *bpos, int regend,
-                     int wsize, int wstep, int alen, int blen, double *out0, double *out1, Run run) {
+                     int wsize, int wstep, int alen, int blen, double *out0, double *out1, uint64_t seed, Run run,
+                     RunP runp = NoPack{}) {
   if (wsize <= 0 || wstep <= 0) return fail(GD_ERR_ARG, "wsize and wstep must be positive");
   if (alen < 0 || blen < 0) return fail(GD_ERR_ARG, "negative array length");
   if (alen == 0 || blen == 0 || regend <= 0) return GD_OK;
@@ -667,6 +795,16 @@ static int host_scan(const double *avals, const double *bvals, const int *apos, 
   if (!ctx) return fail(GD_ERR_HIP, "no HIP device available");
   std::lock_guard<std::mutex> g(ctx->mu);
   HIP_TRY(hipSetDevice(ctx->device));
+  if constexpr (!std::is_same<RunP, NoPack>::value) {
+    gd_chrom one;
+    std::memset(&one, 0, sizeof one);
+    one.alen = alen;
+    one.blen = blen;
+    one.regend = regend;
+    one.seed = seed;
+    st = host_packed(ctx, &one, 1, avals, bvals, apos, bpos, wstep, out0, out1, runp);
+    if (st != GD_HOST_NOPACK) return st;
+  }
   const int64_t nwin = regend / wstep;
   Carve cv{nullptr};
   auto lay = [&](Carve &k, double **av, double **bv, int32_t **ap, int32_t **bp, double **o0, double **o1) {
@@ -697,7 +835,7 @@ static int host_scan(const double *avals, const double *bvals, const int *apos, 
   ch.alen = alen;
   ch.blen = blen;
   ch.regend = regend;
-  ch.seed = g_seed;
+  ch.seed = seed;
   st = run(ctx, &ch, av, bv, ap, bp, o0, o1, s);
   if (st) return st;
   if (nwin > 0) {
@@ -715,9 +853,9 @@ static int css_scan_locked(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, cons
 
 /* several chromosomes from host memory in one device scan: H2D of the inputs and of
  * the caller's outputs (kept at uncomputed windows), the batched scan, D2H */
-template <class Run>
+template <class Run, class RunP = NoPack>
 static int host_batch(const gd_chrom *chroms, int nchrom, const double *avals, const double *bvals, const int *apos,
-                      const int *bpos, int wstep, double *out0, double *out1, Run run) {
+                      const int *bpos, int wstep, double *out0, double *out1, Run run, RunP runp = NoPack{}) {
   if (nchrom < 0 || (nchrom > 0 && !chroms)) return fail(GD_ERR_ARG, "bad chromosome list");
   if (wstep <= 0) return fail(GD_ERR_ARG, "wsize and wstep must be positive");
   int64_t na = 0, nb = 0, nw = 0;
@@ -736,6 +874,10 @@ static int host_batch(const gd_chrom *chroms, int nchrom, const double *avals, c
   if (!ctx) return fail(GD_ERR_HIP, "no HIP device available");
   std::lock_guard<std::mutex> g(ctx->mu);
   HIP_TRY(hipSetDevice(ctx->device));
+  if constexpr (!std::is_same<RunP, NoPack>::value) {
+    st = host_packed(ctx, chroms, nchrom, avals, bvals, apos, bpos, wstep, out0, out1, runp);
+    if (st != GD_HOST_NOPACK) return st;
+  }
   Carve cv{nullptr};
   auto lay = [&](Carve &k, double **av, double **bv, int32_t **ap, int32_t **bp, double **o0, double **o1) {
     *av = k.take<double>(std::max<int64_t>(na, 1));
@@ -778,6 +920,10 @@ extern "C" int gd_fet_scan_host_batch_ex(const gd_chrom *chroms, int nchrom, con
                         hipStream_t s) {
                       return fet_scan_locked(ctx, chroms, nchrom, av, bv, ap, bp, wsize, wstep, perc, mode,
                                              window_set, o0, o1, s);
+                    },
+                    [&](gd_ctx *ctx, const PackedIn &pk, int n, double *o0, double *o1, hipStream_t s) {
+                      return fet_scan_locked(ctx, nullptr, n, nullptr, nullptr, nullptr, nullptr, wsize, wstep, perc,
+                                             mode, window_set, o0, o1, s, &pk);
                     });
 }
 
@@ -792,11 +938,17 @@ extern "C" int gd_css_scan_host_batch_ex(const gd_chrom *chroms, int nchrom, con
                                          const double *bvals, const int *apos, const int *bpos, int wsize, int wstep,
                                          int treshold, int runs, int drosophila, int mds, int window_set,
                                          double *scores, double *p) {
-  return host_batch(chroms, nchrom, avals, bvals, apos, bpos, wstep, scores, p,
-                    [&](gd_ctx *ctx, double *av, double *bv, int32_t *ap, int32_t *bp, double *o0, double *o1,
-                        hipStream_t s) {
-                      return css_scan_locked(ctx, chroms, nchrom, av, bv, ap, bp, wsize, wstep, treshold, runs,
-                                             drosophila, mds, window_set, o0, o1, s);
+  auto ref = [&](gd_ctx *ctx, double *av, double *bv, int32_t *ap, int32_t *bp, double *o0, double *o1,
+                 hipStream_t s) {
+    return css_scan_locked(ctx, chroms, nchrom, av, bv, ap, bp, wsize, wstep, treshold, runs, drosophila, mds,
+                           window_set, o0, o1, s);
+  };
+  if (drosophila) /* allele frequencies, not genotype codes: the reference layout */
+    return host_batch(chroms, nchrom, avals, bvals, apos, bpos, wstep, scores, p, ref);
+  return host_batch(chroms, nchrom, avals, bvals, apos, bpos, wstep, scores, p, ref,
+                    [&](gd_ctx *ctx, const PackedIn &pk, int n, double *o0, double *o1, hipStream_t s) {
+                      return css_scan_locked(ctx, nullptr, n, nullptr, nullptr, nullptr, nullptr, wsize, wstep,
+                                             treshold, runs, 0, mds, window_set, o0, o1, s, &pk);
                     });
 }
 
@@ -812,12 +964,15 @@ extern "C" int gd_fet_scan_host_ex(const double *avals, const double *bvals, con
                                    uint64_t seed, int window_set, double *scores, double *stddev) {
   if (mode != GD_FET_REFERENCE && mode != GD_FET_EXACT)
     return fail(GD_ERR_ARG, "FET mode must be GD_FET_REFERENCE (0) or GD_FET_EXACT (1)");
-  return host_scan(avals, bvals, apos, bpos, regend, wsize, wstep, alen, blen, scores, stddev,
+  return host_scan(avals, bvals, apos, bpos, regend, wsize, wstep, alen, blen, scores, stddev, seed,
                    [&](gd_ctx *ctx, gd_chrom *ch, double *av, double *bv, int32_t *ap, int32_t *bp, double *o0,
                        double *o1, hipStream_t s) {
-                     ch->seed = seed;
                      return fet_scan_locked(ctx, ch, 1, av, bv, ap, bp, wsize, wstep, perc, mode, window_set, o0,
                                             o1, s);
+                   },
+                   [&](gd_ctx *ctx, const PackedIn &pk, int n, double *o0, double *o1, hipStream_t s) {
+                     return fet_scan_locked(ctx, nullptr, n, nullptr, nullptr, nullptr, nullptr, wsize, wstep, perc,
+                                            mode, window_set, o0, o1, s, &pk);
                    });
 }
 
@@ -1028,12 +1183,17 @@ extern "C" int gd_css_scan_host_ex(const double *avals, const double *bvals, con
                                    int regend, int wsize, int wstep, int alen, int blen, int treshold, int runs,
                                    int drosophila, int mds, uint64_t seed, int window_set, double *scores,
                                    double *p) {
-  return host_scan(avals, bvals, apos, bpos, regend, wsize, wstep, alen, blen, scores, p,
-                   [&](gd_ctx *ctx, gd_chrom *ch, double *av, double *bv, int32_t *ap, int32_t *bp, double *o0,
-                       double *o1, hipStream_t s) {
-                     ch->seed = seed;
-                     return css_scan_locked(ctx, ch, 1, av, bv, ap, bp, wsize, wstep, treshold, runs, drosophila,
-                                            mds, window_set, o0, o1, s);
+  auto ref = [&](gd_ctx *ctx, gd_chrom *ch, double *av, double *bv, int32_t *ap, int32_t *bp, double *o0,
+                 double *o1, hipStream_t s) {
+    return css_scan_locked(ctx, ch, 1, av, bv, ap, bp, wsize, wstep, treshold, runs, drosophila, mds, window_set, o0,
+                           o1, s);
+  };
+  if (drosophila) /* allele frequencies, not genotype codes: the reference layout */
+    return host_scan(avals, bvals, apos, bpos, regend, wsize, wstep, alen, blen, scores, p, seed, ref);
+  return host_scan(avals, bvals, apos, bpos, regend, wsize, wstep, alen, blen, scores, p, seed, ref,
+                   [&](gd_ctx *ctx, const PackedIn &pk, int n, double *o0, double *o1, hipStream_t s) {
+                     return css_scan_locked(ctx, nullptr, n, nullptr, nullptr, nullptr, nullptr, wsize, wstep,
+                                            treshold, runs, 0, mds, window_set, o0, o1, s, &pk);
                    });
 }
 
@@ -1042,10 +1202,9 @@ extern "C" int gd_css_coords_host(const double *avals, const double *bvals, cons
                                   int mds, uint64_t seed, int window_set, double *scores, double *p, double *X) {
   if (runs <= 0 || treshold <= 0) return fail(GD_ERR_ARG, "coordinates are kept only for a permutation test");
   if (!X) return fail(GD_ERR_ARG, "null buffer");
-  return host_scan(avals, bvals, apos, bpos, regend, wsize, wstep, alen, blen, scores, p,
+  return host_scan(avals, bvals, apos, bpos, regend, wsize, wstep, alen, blen, scores, p, seed,
                    [&](gd_ctx *ctx, gd_chrom *ch, double *av, double *bv, int32_t *ap, int32_t *bp, double *o0,
                        double *o1, hipStream_t s) {
-                     ch->seed = seed;
                      return css_scan_locked(ctx, ch, 1, av, bv, ap, bp, wsize, wstep, treshold, runs, 0, mds,
                                             window_set, o0, o1, s, nullptr, X);
                    });
@@ -1192,6 +1351,7 @@ extern "C" int gd_set_fet_mode(int mode) {
 }
 extern "C" int gd_get_fet_mode(void) { return g_fet_mode.load(); }
 extern "C" const char *gd_last_error(void) { return g_err.c_str(); }
+extern "C" int gd_last_status(void) { return g_status; }
 extern "C" int gd_device_count(void) {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess) return 0;

@@ -37,6 +37,7 @@
 #include "../../include/gdscan.h"
 
 void gd_set_error(const char *msg); /* gd_api.hip */
+void gd_set_status_error(int code, const char *msg);
 
 struct gd_gtrack {
   std::vector<std::string> seqid;
@@ -350,6 +351,7 @@ struct PRun {
 struct PChunk {
   std::vector<PRun> runs;
   bool ok = true;
+  bool nopack = false; /* a readable track with no packed form (GD_ERR_NOPACK) */
   std::string err;
 };
 
@@ -388,6 +390,7 @@ void parse_packed_chunk(const char *p, const char *end, const Columns &col, PChu
       }
       if (!genotype_code(val, &code)) {
         out->ok = false;
+        out->nopack = true;
         out->err = "a value is not one of the genotype codes 3, 0, -3, -10000: " +
                    std::string(p, (size_t)std::min<ptrdiff_t>(line_end - p, 80));
         return;
@@ -446,7 +449,7 @@ extern "C" gd_ptrack *gd_ptrack_read(const char *path) {
   mt.parallel([&](int k) { parse_packed_chunk(mt.cut[k], mt.cut[k + 1], mt.col, &chunks[k]); });
   for (auto &c : chunks)
     if (!c.ok) {
-      gd_set_error((std::string(path) + ": " + c.err).c_str());
+      gd_set_status_error(c.nopack ? GD_ERR_NOPACK : GD_ERR_ARG, (std::string(path) + ": " + c.err).c_str());
       return nullptr;
     }
   /* merge: the runs of each sequence in file order, their position runs joined */
@@ -487,14 +490,16 @@ extern "C" gd_ptrack *gd_ptrack_read(const char *path) {
   for (int s = 0; s < ns; ++s) {
     const int64_t size = rlen[s][0];
     if (size > INT32_MAX) {
-      gd_set_error((std::string(path) + ": population size above 2^31 in sequence " + t->seqid[s]).c_str());
+      gd_set_status_error(GD_ERR_NOPACK,
+                          (std::string(path) + ": population size above 2^31 in sequence " + t->seqid[s]).c_str());
       return nullptr;
     }
     std::vector<int32_t> &rp = t->rowpos[s];
     rp.reserve((size_t)(nel[s] / size));
     for (size_t j = 0; j < rpos[s].size(); ++j) {
       if (rlen[s][j] % size != 0) {
-        gd_set_error((std::string(path) + ": sequence " + t->seqid[s] + " does not consist of whole rows of " +
+        gd_set_status_error(GD_ERR_NOPACK,
+                            (std::string(path) + ": sequence " + t->seqid[s] + " does not consist of whole rows of " +
                       std::to_string(size) + " individuals at one position (position " +
                       std::to_string(rpos[s][j]) + " holds " + std::to_string(rlen[s][j]) +
                       " elements); such a track keeps the reference layout (gd_gtrack_read)")

@@ -19,6 +19,7 @@ GD_ERR_HIP = -2
 GD_ERR_UNSORTED = -4
 GD_ERR_BOUNDS = -5
 GD_ERR_SIZE = -6
+GD_ERR_NOPACK = -7
 GD_DEFAULT_SEED = 20261015
 GD_WINDOWS_THREADED = 0
 GD_WINDOWS_SERIAL = 1
@@ -36,7 +37,7 @@ EXPORTS = (
     "gd_ctx_create", "gd_ctx_destroy", "gd_window_count",
     "gd_fet_scan_device", "gd_css_scan_device", "gd_css_scan_device_ex", "gd_fet_scan_host_batch",
     "gd_css_scan_host_batch", "gd_css_scan_host_batch_ex",
-    "gd_set_seed", "gd_get_seed", "gd_last_error", "gd_device_count",
+    "gd_set_seed", "gd_get_seed", "gd_last_error", "gd_last_status", "gd_device_count",
     "gd_last_stage_ms", "gd_synth_device",
     "gd_gtrack_read", "gd_gtrack_free", "gd_gtrack_nseq", "gd_gtrack_seqid", "gd_gtrack_len", "gd_gtrack_copy",
     "gd_ptrack_read", "gd_ptrack_free", "gd_ptrack_nseq", "gd_ptrack_seqid", "gd_ptrack_shape", "gd_ptrack_copy",
@@ -44,7 +45,7 @@ EXPORTS = (
     "gd_tabular_read", "gd_tabular_free", "gd_tabular_rows", "gd_tabular_nseq", "gd_tabular_seqid",
     "gd_tabular_copy",
     "gd_fet_region_limit", "gd_css_fdr_threshold", "gd_css_top_limit", "gd_merge_regions",
-    "gd_pack_shape", "gd_pack_chrom", "gd_pack_chrom_device", "gd_fet_scan_packed_device",
+    "gd_pack_shape", "gd_pack_chrom", "gd_pack_chrom_mt", "gd_pack_chrom_device", "gd_fet_scan_packed_device",
     "gd_css_scan_packed_device", "gd_fet_scan_packed_host", "gd_css_scan_packed_host",
 )
 
@@ -167,6 +168,7 @@ def _load() -> C.CDLL:
         getattr(lib, fn).restype = C.c_int
     lib.gd_pack_shape.argtypes = [ip, ip, i32, i32, ip, ip, ip]
     lib.gd_pack_chrom.argtypes = [dp, dp, ip, ip, i32, i32, i32, vp, vp, vp]
+    lib.gd_pack_chrom_mt.argtypes = [dp, dp, ip, ip, i32, i32, i32, vp, vp, vp]
     lib.gd_pack_chrom_device.argtypes = [vp, vp, vp, vp, i32, i32, i32, vp, vp, vp, vp]
     lib.gd_fet_scan_packed_device.argtypes = [vp, C.POINTER(PChrom), i32, vp, vp, vp, i32, i32, C.c_double, i32, i32,
                                               vp, vp, vp]
@@ -175,7 +177,7 @@ def _load() -> C.CDLL:
     lib.gd_fet_scan_packed_host.argtypes = [C.POINTER(PChrom), i32, vp, vp, vp, i32, i32, C.c_double, i32, i32, dp,
                                             dp]
     lib.gd_css_scan_packed_host.argtypes = [C.POINTER(PChrom), i32, vp, vp, vp, i32, i32, i32, i32, i32, i32, dp, dp]
-    for fn in ("gd_pack_shape", "gd_pack_chrom", "gd_pack_chrom_device", "gd_fet_scan_packed_device",
+    for fn in ("gd_pack_shape", "gd_pack_chrom", "gd_pack_chrom_mt", "gd_pack_chrom_device", "gd_fet_scan_packed_device",
                "gd_css_scan_packed_device", "gd_fet_scan_packed_host", "gd_css_scan_packed_host"):
         getattr(lib, fn).restype = C.c_int
     for fn in ("gd_gtrack_nseq", "gd_gtrack_copy", "gd_write_tabular", "gd_format_py2_float", "gd_ptrack_nseq",

@@ -4,6 +4,10 @@
 function (statistics/fisher/fisher_cython_parallel.pyx:14) and its contract:
 float64 avals/bvals, int32 apos/bpos (wrong dtype -> ValueError, as Cython's
 typed buffers raise), outputs written in place at computed windows only.
+
+The bootstrap seed of the reference-signature functions is per calling thread
+(gd_set_seed in one thread does not reach another; include/gdscan.h): a worker thread
+sets its own, or calls scan(..., seed=...).
 """
 from __future__ import annotations
 

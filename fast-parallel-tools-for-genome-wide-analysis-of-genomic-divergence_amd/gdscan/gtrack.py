@@ -16,7 +16,7 @@ from collections import OrderedDict
 
 import numpy as np
 
-from ._lib import GdError, check, lib
+from ._lib import GD_ERR_NOPACK, GdError, check, lib
 
 # VCFConvert.py:9-18
 GT_VALUES = {"./.": -10000, ".|.": -10000, "1/0": 0, "0/1": 0, "1|0": 0, "0|1": 0, "0/0": 3, "0|0": 3,
@@ -49,9 +49,10 @@ def read_gtrack_packed(path) -> "OrderedDict[str, tuple[np.ndarray, np.ndarray, 
     h = lib.gd_ptrack_read(str(path).encode())
     if not h:
         msg = lib.gd_last_error().decode(errors="replace")
-        if "genotype codes" in msg or "whole rows" in msg:
+        st = lib.gd_last_status()
+        if st == GD_ERR_NOPACK:  # readable, but no packed form: callers fall back to read_gtrack
             raise ValueError(msg)
-        raise GdError(-1, msg)
+        raise GdError(st, msg)
     try:
         out = OrderedDict()
         size, nrows = C.c_int32(), C.c_int64()

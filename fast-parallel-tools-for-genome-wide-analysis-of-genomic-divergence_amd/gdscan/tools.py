@@ -8,6 +8,10 @@ Differences from the Galaxy tools: chromosomes come in the order track A lists t
 (HyperBrowser iterates the genome's chromosome list); the region of a chromosome is
 [0, chrom_lengths[seqid]) when given, else [0, last position + 1) (HyperBrowser uses
 the genome build's chromosome length).
+
+Seeds: every chromosome's bootstrap / permutation stream derives from `seed` (default: the
+calling thread's gd_set_seed value -- the library keeps one seed per thread, so a worker
+thread that should follow the main thread's setting passes seed= explicitly).
 """
 from __future__ import annotations
 
@@ -17,7 +21,11 @@ from ._lib import GD_WINDOWS_THREADED, Chrom, check, lib
 from .gtrack import read_gtrack, write_tabular
 
 
-def _batch(track_a, track_b, wstep, chrom_lengths):
+def _seed(seed):
+    return lib.gd_get_seed() if seed is None else int(seed)
+
+
+def _batch(track_a, track_b, wstep, chrom_lengths, seed=None):
     ta, tb = read_gtrack(track_a), read_gtrack(track_b)
     names = [s for s in ta if s in tb and len(ta[s][0]) > 0]
     chroms = (Chrom * max(len(names), 1))()
@@ -30,7 +38,7 @@ def _batch(track_a, track_b, wstep, chrom_lengths):
         chroms[c].a_off, chroms[c].b_off = off_a, off_b
         chroms[c].alen, chroms[c].blen = len(va), len(vb)
         chroms[c].regend, chroms[c].w_out = regend, w
-        chroms[c].seed = lib.gd_get_seed()
+        chroms[c].seed = _seed(seed)
         av.append(va); bv.append(vb); ap.append(pa); bp.append(pb)
         off_a += len(va); off_b += len(vb); w += regend // wstep
     cat = lambda xs, dt: np.ascontiguousarray(np.concatenate(xs) if xs else np.zeros(0), dtype=dt)
@@ -68,21 +76,22 @@ def _ptr(a, ct):
 
 
 def fisher_exact_test_snp(track_a, track_b, out_path, wsize=2500, wstep=500, percentile=0.95, chrom_lengths=None,
-                          exact=None, packed="auto"):
+                          exact=None, packed="auto", seed=None):
     """packed: "auto" reads genotype tracks straight into 2-bit codes (gdscan.packed; same
     windows, scores and bootstrap streams) and falls back to the reference layout for
-    tracks with no packed form; True requires the packed form, False never uses it."""
+    tracks with no packed form; True requires the packed form, False never uses it.
+    seed: the bootstrap seed (None: this thread's gd_set_seed value)."""
     import ctypes as C
     pair = _packed_pair(track_a, track_b, chrom_lengths, packed)
     if pair is not None:
         from . import packed as pk
         names, pcs = pair
-        res = pk.fet_scan(pcs, wsize, wstep, percentile, exact=exact) if names else []
+        res = pk.fet_scan(pcs, wsize, wstep, percentile, seed=_seed(seed), exact=exact) if names else []
         scores = np.concatenate([r[0] for r in res]) if res else np.zeros(0)
         stddev = np.concatenate([r[1] for r in res]) if res else np.zeros(0)
         _write(out_path, "#seqid\tstart\tscore\tstddev", names, [p.regend for p in pcs], wstep, scores, stddev)
         return names, scores, stddev
-    names, chroms, av, bv, ap, bp, w = _batch(track_a, track_b, wstep, chrom_lengths)
+    names, chroms, av, bv, ap, bp, w = _batch(track_a, track_b, wstep, chrom_lengths, seed)
     scores, stddev = np.zeros(w), np.zeros(w)
     if names:
         mode = lib.gd_get_fet_mode() if exact is None else int(bool(exact))  # GD_FET_REFERENCE / GD_FET_EXACT
@@ -101,12 +110,13 @@ MDS = {"classical": 0, "Classical MDS": 0, "smacof": 1, "SMACOF": 1, "smacof+cmd
 
 
 def cluster_separation_score(track_a, track_b, out_path, wsize=2500, wstep=500, mc_treshold=10, mc_runs=0,
-                             compare="count", mds="classical", chrom_lengths=None, packed="auto"):
+                             compare="count", mds="classical", chrom_lengths=None, packed="auto", seed=None):
     """compare: "count" (SNP differences) or "freq" (drosophila allele-frequency metric,
     one frequency track per population); mds: "classical", "smacof" or "smacof+cmds"
     (any other label selects SMACOF + classical, as the tool's else branch does);
     packed: as fisher_exact_test_snp (the count metric only: "freq" tracks hold
-    frequencies, never genotype codes)."""
+    frequencies, never genotype codes); seed: the permutation seed (None: this thread's
+    gd_set_seed value)."""
     import ctypes as C
     if compare not in COMPARE:
         raise ValueError(f"unknown distance metric {compare!r}")
@@ -117,12 +127,12 @@ def cluster_separation_score(track_a, track_b, out_path, wsize=2500, wstep=500, 
     if pair is not None:
         from . import packed as pk
         names, pcs = pair
-        res = pk.css_scan(pcs, wsize, wstep, mc_treshold, mc_runs, md) if names else []
+        res = pk.css_scan(pcs, wsize, wstep, mc_treshold, mc_runs, md, seed=_seed(seed)) if names else []
         scores = np.concatenate([r[0] for r in res]) if res else np.zeros(0)
         p = np.concatenate([r[1] for r in res]) if res else np.zeros(0)
         _write(out_path, "#seqid\tstart\tscore\tp", names, [c.regend for c in pcs], wstep, scores, p)
         return names, scores, p
-    names, chroms, av, bv, ap, bp, w = _batch(track_a, track_b, wstep, chrom_lengths)
+    names, chroms, av, bv, ap, bp, w = _batch(track_a, track_b, wstep, chrom_lengths, seed)
     scores, p = np.zeros(w), np.zeros(w)
     if names:
         check(lib.gd_css_scan_host_batch_ex(chroms, len(names), _ptr(av, C.c_double), _ptr(bv, C.c_double),

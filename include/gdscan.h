@@ -42,6 +42,7 @@ extern "C" {
 #define GD_ERR_UNSORTED (-4) /* positions not non-decreasing (slide_right assumes sorted) */
 #define GD_ERR_BOUNDS (-5)   /* a window's B slice runs past blen (reference: out-of-bounds read) */
 #define GD_ERR_SIZE (-6)     /* empty population / unsupported window size */
+#define GD_ERR_NOPACK (-7)   /* a readable track with no packed form (gd_ptrack_read; keeps the reference layout) */
 
 #define GD_DEFAULT_SEED 20261015ULL
 
@@ -182,6 +183,10 @@ int gd_pack_shape(const int *apos, const int *bpos, int alen, int blen, int *asi
  * reference layout (gd_*_scan_*). */
 int gd_pack_chrom(const double *avals, const double *bvals, const int *apos, const int *bpos, int asize, int bsize,
                   int nrows, uint64_t *acodes, uint64_t *bcodes, int32_t *rowpos);
+/* the same on host threads (GD_HOST_THREADS, else the CPU affinity capped by OMP_NUM_THREADS and
+ * 16): what the reference-signature host entry points use before anything crosses PCIe */
+int gd_pack_chrom_mt(const double *avals, const double *bvals, const int *apos, const int *bpos, int asize,
+                     int bsize, int nrows, uint64_t *acodes, uint64_t *bcodes, int32_t *rowpos);
 /* the same on the device (device pointers; a reference-layout track already in HBM) */
 int gd_pack_chrom_device(const double *avals, const double *bvals, const int32_t *apos, const int32_t *bpos,
                          int asize, int bsize, int nrows, uint64_t *acodes, uint64_t *bcodes, int32_t *rowpos,
@@ -236,6 +241,7 @@ void gd_set_seed(uint64_t seed);     /* seed used by the reference-signature ent
                                        calling thread (thread-local; every thread starts at GD_DEFAULT_SEED) */
 uint64_t gd_get_seed(void);          /* the calling thread's seed */
 const char *gd_last_error(void);     /* thread-local message for the last failing call */
+int gd_last_status(void);            /* thread-local status (GD_ERR_*) that went with that message */
 int gd_device_count(void);
 
 /* timing of the last device scan on this thread (ms, HIP events on the scan's
@@ -267,9 +273,10 @@ int gd_gtrack_copy(const gd_gtrack *t, int s, int32_t *starts, double *vals);
 /* the same files parsed straight into packed genotype tracks (2-bit codes, one position
  * per row; no f64 intermediate): per sequence, size = get_population_size() (the leading
  * run of equal positions, comparative.c:25-34) and nrows rows of `size` individuals at one
- * position.  NULL (gd_last_error) for a track with no packed form -- a value other than
- * 3, 0, -3, -10000, or a sequence whose positions do not come in whole rows -- which keeps
- * the reference layout (gd_gtrack_read).  A pair of tracks scans packed (gd_pchrom) when
+ * position.  NULL (gd_last_error) on failure; gd_last_status() is GD_ERR_NOPACK for a
+ * readable track with no packed form -- a value other than 3, 0, -3, -10000, a sequence whose
+ * positions do not come in whole rows, a population above 2^31 -- which keeps the reference
+ * layout (gd_gtrack_read).  A pair of tracks scans packed (gd_pchrom) when
  * each shared sequence has the same rowpos in both. */
 typedef struct gd_ptrack gd_ptrack;
 gd_ptrack *gd_ptrack_read(const char *path);
