@@ -13,6 +13,15 @@ from conftest import close, oracle_fet_scan
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True, params=["host_packed", "reference_layout"])
+def _host_route(request, monkeypatch):
+    """every host-API test twice: the drop-in calls pack whole-row genotype tracks on the host
+    (gd_api.hip host_packed) -- and once with that route off, so the reference-layout device
+    scan (self bounds, the window kernel's own ranges) sees the same inputs"""
+    if request.param == "reference_layout":
+        monkeypatch.setenv("GD_HOST_NOPACK", "1")
+
+
 def _synth(c, nsnp, a, b):
     from gdscan import synth
     return synth.chromosome(c, nsnp, a, b)
