@@ -29,10 +29,11 @@ def _cmp_scores(s, s_ref, rel=1e-9):
 
 @pytest.mark.parametrize("asize,bsize,nsnp", [(10, 10, 60_000), (20, 20, 30_000), (7, 13, 30_000), (40, 40, 4_000),
                                               (1, 1, 20_000), (33, 31, 6_000), (45, 45, 3_000),
-                                              # the two-windows-per-wave p40 tier below m = 40: partial rows
-                                              # of window B in lanes 40-63 and in the LDS tail quads
-                                              (12, 13, 8_000), (15, 16, 8_000), (16, 17, 8_000), (19, 20, 8_000),
-                                              (13, 14, 8_000), (5, 30, 8_000),
+                                              # the two-windows-per-wave 40 tier below m = 40: rows 0-31 of
+                                              # each window in its half wave, rows 32-39 in the LDS tail quads
+                                              # (m = 25, 31, 32: no tail row; 33: one; 34, 35, 39)
+                                              (12, 13, 8_000), (15, 16, 8_000), (16, 16, 8_000), (16, 17, 8_000),
+                                              (17, 17, 8_000), (19, 20, 8_000), (13, 14, 8_000), (5, 30, 8_000),
                                               # the one-wave 80 tier: 1, 8 and 9 tail rows (m = 65, 72, 73)
                                               (33, 32, 3_000), (30, 42, 3_000), (43, 30, 3_000)])
 def test_scores_match_oracle(oracle, asize, bsize, nsnp):
