@@ -3000,15 +3000,12 @@ __global__ void __launch_bounds__(64, CSS_P40_WAVES)
   __shared__ __attribute__((aligned(16))) double s_d[2][MP + 4];
   __shared__ double s_e[2][MP], s_tau[2][MP];
   __shared__ double s_x[2][2 * MP];
-  __shared__ int s_tr[MP];
   __shared__ double s_lam[2][2];
-  __shared__ double s_red[4];
 
   const int lane = threadIdx.x;
   const bool h = lane >= 32;
   const int hi = h ? 1 : 0, r = lane & 31;
   const int tr = r >> 2, tq = lane & 3, R = H40_MAIN + tr;
-  if (lane < MP) s_tr[lane] = lane;
 
   /* the two windows' bookkeeping (uniform) */
   int64_t W[2];
@@ -3469,21 +3466,40 @@ __global__ void __launch_bounds__(64, CSS_P40_WAVES)
     }
     __syncthreads();
   }
-#pragma unroll
-  for (int x = 0; x < 2; ++x) {
-    if (M[x] == 0) continue;
-    const double *X = s_x[x];
-    const double score = css_score<1>(s_tr, Aa[x], Bb[x], [&](int p, int q) { return xdist(X, p, q); }, s_red);
-    if (score == -1.0) continue; /* the reference's "discarded" marker (css.c:127) */
-    const gd_chrom_dev &d = ch[C[x]];
-    const int64_t wl = W[x] - d.w_base;
-    if (lane == 0) {
-      scores[d.w_out + wl] = score;
-      if (!want_x) pvals[d.w_out + wl] = 1.0; /* runs == 0: p = (0 + 1) / (0 + 1) */
+  /* css (css.c:608-647) of both windows at once, each over its own half: the pairs of
+   * css_score spread over 32 lanes instead of 64, one half-wave sum for both */
+  {
+    const int a = h ? Aa[1] : Aa[0], b = h ? Bb[1] : Bb[0], m = h ? M[1] : M[0];
+    const double *X = s_x[hi];
+    const int ab = a * b;
+    const float invb = 1.0f / (float)b;
+    double bet = 0.0, win = 0.0;
+    if (m > 0) {
+      for (int q = r; q < ab; q += 32) {
+        const int ii = (int)(((float)q + 0.5f) * invb); /* exact for q < 2^14 (ab <= 400 here) */
+        bet += xdist(X, ii, a + (q - ii * b));
+      }
+      /* consecutive pairs only (Q8), each pre-divided by its group's a^2 (a-1) */
+      for (int k = r; k < m - 1; k += 32) {
+        if (k < a - 1) win += xdist(X, k, k + 1) / (double)(a * a * (a - 1));
+        if (k >= a) win += xdist(X, k, k + 1) / (double)(b * b * (b - 1));
+      }
     }
-    if (want_x) {
-      for (int e = lane; e < 2 * MP; e += 64) xbuf[W[x] * 2 * MP + e] = (e < 2 * M[x]) ? X[e] : 0.0;
-      if (lane == 0) status[W[x]] = 1;
+    half_sum2(bet, win);
+    const double score = bet / (a * b) - (a + b) * win;
+    /* score == -1: the reference's "discarded" marker (css.c:127) */
+    if (m > 0 && score != -1.0) {
+      const int64_t w = h ? W[1] : W[0];
+      const gd_chrom_dev &d = ch[h ? C[1] : C[0]];
+      const int64_t wl = w - d.w_base;
+      if (r == 0) {
+        scores[d.w_out + wl] = score;
+        if (!want_x) pvals[d.w_out + wl] = 1.0; /* runs == 0: p = (0 + 1) / (0 + 1) */
+      }
+      if (want_x) {
+        for (int e = r; e < 2 * MP; e += 32) xbuf[w * 2 * MP + e] = (e < 2 * m) ? X[e] : 0.0;
+        if (r == 0) status[w] = 1;
+      }
     }
   }
   CSS_PROF(6);
