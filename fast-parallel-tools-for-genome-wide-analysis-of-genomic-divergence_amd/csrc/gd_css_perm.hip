@@ -39,21 +39,30 @@
 #define PERM_OPAQUE(x) asm volatile("" : "+v"(x))
 
 #ifdef GD_PERM_PROFILE
-/* diagnostics build only: shader-clock cycles per phase summed over workgroups (thread 0) */
+/* diagnostics build only: shader-clock cycles per phase summed over workgroups (thread 0),
+ * accumulated in registers and added to the global totals once per workgroup at exit (an
+ * atomic per phase boundary queued behind every other workgroup's and then held up the
+ * next vmcnt wait, the work queue's, which showed as queue time) */
 #include <cstdio>
 __device__ unsigned long long g_perm_prof[8];
-#define PERM_PROF_INIT uint64_t prof_t = __builtin_readcyclecounter()
-#define PERM_PROF(ph)                                                  \
-  do {                                                                 \
-    if (threadIdx.x == 0) {                                            \
-      const uint64_t t_ = __builtin_readcyclecounter();               \
-      atomicAdd(&g_perm_prof[ph], (unsigned long long)(t_ - prof_t)); \
-      prof_t = t_;                                                     \
-    }                                                                  \
+#define PERM_PROF_INIT                                  \
+  uint64_t prof_t = __builtin_readcyclecounter();      \
+  uint64_t prof_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}
+#define PERM_PROF(ph)                                  \
+  do {                                                 \
+    const uint64_t t_ = __builtin_readcyclecounter(); \
+    prof_acc[ph] += t_ - prof_t;                       \
+    prof_t = t_;                                       \
+  } while (0)
+#define PERM_PROF_FLUSH                                                                           \
+  do {                                                                                            \
+    if (threadIdx.x == 0)                                                                         \
+      for (int ph_ = 0; ph_ < 8; ++ph_) atomicAdd(&g_perm_prof[ph_], (unsigned long long)prof_acc[ph_]); \
   } while (0)
 #else
 #define PERM_PROF_INIT
 #define PERM_PROF(ph)
+#define PERM_PROF_FLUSH
 #endif
 
 namespace {
@@ -895,8 +904,12 @@ __global__ void __launch_bounds__(PermShape<MP>::NT) PERM_WPE
     if (tid == 0) s_w = (int64_t)atomicAdd(wq, 1u);
     __syncthreads();
     const int64_t w = s_w;
-    if (w >= wtotal) break;
+    if (w >= wtotal) {
+      PERM_PROF_FLUSH;
+      break;
+    }
     if (!status[w]) continue;
+    PERM_PROF(5); /* work queue and status */
     const int c = perm_chrom_of(ch, nchrom, w);
     const gd_chrom_dev &d = ch[c];
     const int a = d.asize, b = d.bsize, m = a + b, m1 = m - 1;
@@ -928,6 +941,7 @@ __global__ void __launch_bounds__(PermShape<MP>::NT) PERM_WPE
         y0 = fmin(y0, __shfl_xor(y0, o));
         y1 = fmax(y1, __shfl_xor(y1, o));
       }
+      PERM_PROF(7); /* the coordinates and their bounding box */
       const double dmax = sqrt((x1 - x0) * (x1 - x0) + (y1 - y0) * (y1 - y0));
       int ex = 0;
       if (dmax > 0.0) (void)frexp(dmax, &ex);
@@ -946,6 +960,7 @@ __global__ void __launch_bounds__(PermShape<MP>::NT) PERM_WPE
         }
         *reinterpret_cast<_Float16 *>(s_U + row * SH::RS + 2 * k) = (_Float16)v;
       }
+      PERM_PROF(6); /* the fp16 matrix */
       const gd_randint rb = perm_rd((uint32_t)(b > 1 ? b : 2), s_mag[b > 1 ? b : 2]);
       obs = score_exact_wave<MP>([](int k) { return (uint32_t)k; }, s_X, a, b, inva, invb, lane, my_lst, rb);
       if (tid < m) s_car[tid] = (uint8_t)tid; /* tracks := identity */
@@ -1505,8 +1520,10 @@ int gd_css_perm_launch(int mp, const gd_chrom_dev *d_ch, int nchrom, const doubl
       unsigned long long h[8];
       (void)hipStreamSynchronize(s);
       (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(g_perm_prof), sizeof h);
-      fprintf(stderr, "perm-prof cycles: setup %llu draws %llu compose %llu score %llu hits %llu\n", h[0], h[1], h[2],
-              h[3], h[4]);
+      fprintf(stderr,
+              "perm-prof cycles: setup %llu draws %llu compose %llu score %llu hits %llu (setup parts: queue+status %llu "
+              "coordinates %llu fp16 matrix %llu; the rest is the observed score)\n",
+              h[0], h[1], h[2], h[3], h[4], h[5], h[7], h[6]);
     }
   } dump{s};
 #endif
