@@ -57,7 +57,7 @@ MFMA_I8_PEAK_TOPS = 5000.0  # MI355X_MICROARCH.md: I8 MFMA at 2x the BF16 rate (
 # tools/ubench_valu.hip: v_lshrrev_b32, v_add_f32, v_max_u16 ... 880-994 G/s at the held ~2.1 GHz).
 # Multiplies, FP64 and VOP3 three-source ops are 4-cycle: a kernel made of them tops out at 0.5.
 VALU_PEAK_GINSTS = 1024 * 2.4 / 2
-PROFILE_ROUND = "r04"
+PROFILE_ROUND = "r05"
 PROF = ROOT / "profiles"
 TRAFFIC_FILE = PROF / f"{PROFILE_ROUND}_fet_traffic.json"
 VALU_FILE = PROF / f"{PROFILE_ROUND}_fet_valu.json"

@@ -37,16 +37,21 @@
 #include "gd_internal.h"
 
 #ifdef GD_CSS_PROFILE
-/* diagnostics build only: shader-clock cycles per phase summed over windows (lane 0) */
+/* diagnostics build only: shader-clock cycles per phase summed over windows (lane 0),
+ * accumulated in registers and added to the totals at the last phase (6): a global atomic
+ * at every phase boundary would hold up the next vector-memory wait (the counters drain in
+ * order) and bill its queueing to the following phase */
 __device__ unsigned long long g_css_prof[8];
-#define CSS_PROF_INIT uint64_t prof_t = __builtin_readcyclecounter()
-#define CSS_PROF(ph)                                                  \
-  do {                                                                \
-    if (threadIdx.x == 0) {                                           \
-      const uint64_t t_ = __builtin_readcyclecounter();              \
-      atomicAdd(&g_css_prof[ph], (unsigned long long)(t_ - prof_t)); \
-      prof_t = t_;                                                    \
-    }                                                                 \
+#define CSS_PROF_INIT                             \
+  uint64_t prof_t = __builtin_readcyclecounter(); \
+  uint64_t prof_acc[7] = {0, 0, 0, 0, 0, 0, 0}
+#define CSS_PROF(ph)                                                                             \
+  do {                                                                                           \
+    const uint64_t t_ = __builtin_readcyclecounter();                                           \
+    prof_acc[ph] += t_ - prof_t;                                                                 \
+    prof_t = t_;                                                                                 \
+    if ((ph) == 6 && threadIdx.x == 0)                                                           \
+      for (int ph_ = 0; ph_ < 7; ++ph_) atomicAdd(&g_css_prof[ph_], (unsigned long long)prof_acc[ph_]); \
   } while (0)
 #else
 #define CSS_PROF_INIT

@@ -135,6 +135,7 @@ def test_bench_two_ranks_one_gpu():
     out = json.loads(so.strip().splitlines()[-1])
     assert out["n_gpus"] == 2 and out["config"]["collective_backend"] == "gloo"
     assert out["config"]["track_gather_ms"] is not None
+    assert out["cpu_baseline"]["value"] > 0  # rank 0 times the reference CPU path at N > 1 too
     c5 = out["css"]["c5"]
     assert sum(c5["chromosomes_per_rank"]) == 4 and c5["track_gather_ms"] is not None
     assert c5["permutations"]["total"] > 0
