@@ -1009,7 +1009,7 @@ def main():
     sources = {}
     roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, "traffic": None, "alg_bytes_per_step": alg_bytes,
-            "kernel_ms": kernel_ms, "kernel": "whole scan: k_popsize, k_bounds, k_fet_window_fast (HIP events)"}
+            "kernel_ms": kernel_ms, "kernel": "whole scan: k_fet_setup, k_bounds, k_fet_window_fast (HIP events)"}
     if TRAFFIC_FILE.exists():
         tr = json.loads(TRAFFIC_FILE.read_text())
         if tr.get("config") == [nch, nsnp, a, b]:

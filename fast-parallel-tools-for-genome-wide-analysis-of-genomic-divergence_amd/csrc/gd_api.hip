@@ -551,6 +551,13 @@ static int fet_scan_locked(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, cons
   HIP_TRY(hipEventRecord(ctx->ev[1], sm)); /* end of the prologue */
   std::vector<int> cuts(G + 1);
   for (int g = 0; g <= G; ++g) cuts[g] = (int)((int64_t)nchrom * g / G);
+  if (const char *e0 = getenv("GD_GROUP0")) { /* diagnostics: the first group's chromosomes, the rest split evenly */
+    const int n0 = std::max(1, std::min(nchrom - (G - 1), atoi(e0)));
+    if (G > 1) {
+      cuts[1] = n0;
+      for (int g = 2; g <= G; ++g) cuts[g] = n0 + (int)((int64_t)(nchrom - n0) * (g - 1) / (G - 1));
+    }
+  }
   auto bounds_pass = [&](int g) -> int {
     const int c0 = cuts[g], nc = cuts[g + 1] - cuts[g];
     int64_t amax = 1, mx = 1;

@@ -66,6 +66,12 @@ def need(per, names, where):
         raise SystemExit(f"{where}: kernels {missing} absent from the counters (have {sorted(per)})")
 
 
+def valu_busy(c):
+    """VALU-active fraction of the SIMD-cycles while the kernel ran"""
+    g = c.get("GRBM_GUI_ACTIVE", 0.0)
+    return 4.0 * c["SQ_ACTIVE_INST_VALU"] / (1024.0 * g / 8.0) if g > 0 else None
+
+
 def last_json(path):
     for line in reversed(Path(path).read_text().strip().splitlines()):
         if line.startswith("{"):
@@ -133,8 +139,8 @@ ub = {"peak_ginsts": peak, "method": "tools/ubench_valu.hip on the box: median i
 # ---- FET HBM traffic and VALU per scan
 fetch, nf = counters(src / "pmc_fetch")
 write, _ = counters(src / "pmc_write")
-need(fetch, ["k_popsize", "k_bounds", "k_fet_window_fast"], "pmc_fetch")
-scans = nf["k_popsize"]
+need(fetch, ["k_fet_setup", "k_bounds", "k_fet_window_fast"], "pmc_fetch")
+scans = nf["k_fet_setup"]
 fk = {k: v["FETCH_SIZE"] for k, v in fetch.items() if k.startswith(FET_KERNELS)}
 wk = {k: v["WRITE_SIZE"] for k, v in write.items() if k.startswith(FET_KERNELS)}
 # rocprofv3 reports FETCH_SIZE / WRITE_SIZE in KiB; gfx950 FETCH_SIZE counts half of a wide
@@ -154,8 +160,8 @@ traffic = {
 (dst / f"{R}_fet_traffic.json").write_text(json.dumps(traffic, indent=1) + "\n")
 
 valu, nv = counters(src / "pmc_valu")
-need(valu, ["k_popsize", "k_bounds", "k_fet_window_fast"], "pmc_valu")
-vscans = nv["k_popsize"]
+need(valu, ["k_fet_setup", "k_bounds", "k_fet_window_fast"], "pmc_valu")
+vscans = nv["k_fet_setup"]
 vk = {k: v for k, v in valu.items() if k.startswith(FET_KERNELS)}
 valu_doc = {
     "config": config,
@@ -171,12 +177,6 @@ valu_doc = {
 
 # ---- CSS legs: wave-instructions per window of the kernels each leg dispatches
 css_doc = {}
-
-
-def valu_busy(c):
-    """VALU-active fraction of the SIMD-cycles while the kernel ran"""
-    g = c.get("GRBM_GUI_ACTIVE", 0.0)
-    return 4.0 * c["SQ_ACTIVE_INST_VALU"] / (1024.0 * g / 8.0) if g > 0 else None
 
 
 def css_entry(key, d, kernels, windows, what):
@@ -282,11 +282,13 @@ lines += ["", f"VALU ceiling used by every fraction (bench.py VALU_PEAK_GINSTS):
           f"(fetch {fetch_b / 1e9:.3f} + write {write_b / 1e9:.3f}); algorithmic B = {alg / 1e9:.3f} GB.",
           "", f"FET scan VALU (PMC SQ_INSTS_VALU): {valu_doc['valu_wave_insts_per_scan'] / 1e9:.3f} G wave-instructions "
           f"per scan = {fet_gi:.0f} G/s at the bench's scan time ({scan_ms:.3f} ms) = {fet_gi / VPEAK:.3f} of the ceiling"
-          + (f"; k_fet_window_fast VALU busy (4 SQ_ACTIVE_INST_VALU / (1024 x GRBM_GUI_ACTIVE / 8)) {wbusy:.3f}."
+          + (f"; k_fet_window_fast VALU-active share {wbusy:.3f} (4 SQ_ACTIVE_INST_VALU / (1024 SIMDs x GRBM_GUI_ACTIVE / 8): "
+             "the cycles a wave has a VALU instruction in flight per SIMD-cycle -- pipelined instructions of several "
+             "waves overlap, so ~1 means the VALU never waits for work, not a fraction of a ceiling)."
              if wbusy else "."), ""]
 for k, v in css_doc.items():
     lines.append(f"CSS {k}: {v['valu_wave_insts_per_window']:.0f} VALU wave-instructions per window "
-                 f"({' + '.join(v['kernels'])}); VALU busy "
+                 f"({' + '.join(v['kernels'])}); VALU-active share "
                  + ", ".join(f"{kk} {bb:.3f}" for kk, bb in v["valu_busy"].items() if bb is not None) + "."
                  + (f" Matrix cores: {v['mfma']['mfma_per_dispatch'] / 1e6:.1f} M v_mfma_f32_32x32x16_f16 per "
                     f"dispatch, {100 * v['mfma']['frac']:.1f} % of the SIMD-cycles busy." if "mfma" in v else ""))
