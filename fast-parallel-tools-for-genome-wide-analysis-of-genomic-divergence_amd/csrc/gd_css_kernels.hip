@@ -80,6 +80,9 @@ __device__ unsigned long long g_css_prof[8];
 #ifndef CSS_H40
 #define CSS_H40 1 /* the 25-40 tier with one window per half wave (k_css_mds_h40; 0: k_css_mds_p40) */
 #endif
+#ifndef CSS_H40_FUSED
+#define CSS_H40_FUSED 1 /* k_css_mds_h40 with t80's fused Householder step (0: the publish-row form) */
+#endif
 #ifndef CSS_T80
 #define CSS_T80 1 /* the 80-individual tier in one wave with an LDS tail (k_css_mds_t80) */
 #endif
@@ -2979,6 +2982,212 @@ struct H40Steps<P40> {
                                              double (*)[P40], double (*)[P40 + 4], double (*)[P40], double (*)[P40],
                                              double (*)[8][H40_TSTRIDE]) {}
 };
+
+/* The fused Householder step of k_css_mds_t80 on each half wave (CSS_H40_FUSED): row K of
+ * each window is read as column K -- every lane carries its own entry of it and p = A r from
+ * the previous pass (H40Carry) --, so a step is one half-wave sum, the scalars, one LDS round
+ * trip of (v_i, w_i) and the next column, and one pass over the row that applies the rank-2
+ * update and accumulates the next step's p.  The unfused h40_step publishes row K from one
+ * lane first and takes two LDS round trips and two passes. */
+struct H40Carry {
+  double r, p, rt, pt; /* column K entry and p_i of this lane's main row and tail row */
+};
+
+template <int K>
+__device__ __forceinline__ void h40_fused_pass(double (&A)[P40], double vi, double wi, double vt, double wt,
+                                               const double2 *s_vw, const double *s_r,
+                                               double (*s_tail)[H40_TSTRIDE], H40Carry &c) {
+  constexpr int MP = P40;
+  const int lane = css_lane_now(), tr = (lane & 31) >> 2, tq = lane & 3;
+  double p[4] = {0.0, 0.0, 0.0, 0.0};
+  constexpr int FB = 4; /* columns per pinned group */
+  constexpr int NB = MP / FB, JB0 = (K + 1) / FB;
+  double2 cvw[FB];
+  double cr[FB];
+#pragma unroll
+  for (int u = 0; u < FB; ++u) {
+    cvw[u] = s_vw[FB * JB0 + u];
+    cr[u] = s_r[FB * JB0 + u];
+  }
+#pragma unroll
+  for (int jb = JB0; jb < NB; ++jb) {
+    double2 nvw[FB];
+    double nr[FB];
+    if (jb + 1 < NB) {
+#pragma unroll
+      for (int u = 0; u < FB; ++u) {
+        nvw[u] = s_vw[FB * (jb + 1) + u];
+        nr[u] = s_r[FB * (jb + 1) + u];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < FB; ++u) {
+      const int j = FB * jb + u;
+      if (j > K) A[j] = fma(-vi, cvw[u].y, fma(-wi, cvw[u].x, A[j]));
+    }
+#pragma unroll
+    for (int u = 0; u < FB; ++u) CSS_PIN(A[FB * jb + u]);
+#pragma unroll
+    for (int u = 0; u < FB; ++u) {
+      const int j = FB * jb + u;
+      if (j > K + 1) p[u & 3] = fma(A[j], cr[u], p[u & 3]);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) CSS_PIN(p[u]);
+    if (jb + 1 < NB) {
+#pragma unroll
+      for (int u = 0; u < FB; ++u) {
+        cvw[u] = nvw[u];
+        cr[u] = nr[u];
+      }
+    }
+  }
+  A[K] = vi; /* stash v_K in the dead column K */
+  double *tw = s_tail[tr];
+  double t0 = 0.0, t1 = 0.0;
+#pragma unroll
+  for (int s = 0; s < H40_TS; ++s) {
+    if (4 * s + 3 > K) { /* v_j = w_j = 0 at j <= K: the dead columns stay */
+      const int j = 4 * s + tq;
+      const double2 vw = s_vw[j];
+      const double t = fma(-vt, vw.y, fma(-wt, vw.x, tw[j]));
+      tw[j] = t;
+      if (s & 1)
+        t1 = fma(t, s_r[j], t1);
+      else
+        t0 = fma(t, s_r[j], t0);
+    }
+  }
+  if (tq == (K & 3)) tw[K] = vt;
+  c.p = (p[0] + p[1]) + (p[2] + p[3]);
+  c.pt = quad_sum(t0 + t1);
+}
+
+/* column 0 and p = A r before step 0 */
+__device__ __forceinline__ void h40_fused_start(const double (&A)[P40], double (*s_r)[P40 + 2], double (*s_d)[P40 + 4],
+                                                double (*s_tail)[8][H40_TSTRIDE], H40Carry &c) {
+  constexpr int MP = P40;
+  const int lane = css_lane_now(), hi = lane >> 5, r = lane & 31, tr = r >> 2, tq = lane & 3, R = H40_MAIN + tr;
+  c.r = A[0];
+  c.rt = s_tail[hi][tr][0];
+  __syncthreads();
+  s_r[hi][r] = r > 0 ? c.r : 0.0;
+  if (tq == 0) s_r[hi][R] = c.rt;
+  if (r == 0) s_d[hi][0] = c.r;
+  __syncthreads();
+  const double *sr = s_r[hi];
+  double p[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int j = 1; j < MP; ++j) {
+    p[j & 3] = fma(A[j], sr[j], p[j & 3]);
+    if ((j & 7) == 7) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) CSS_PIN(p[u]);
+    }
+  }
+  const double *trw = s_tail[hi][tr];
+  double t0 = 0.0, t1 = 0.0;
+#pragma unroll
+  for (int s = 0; s < H40_TS; ++s) {
+    const int j = 4 * s + tq;
+    if (s & 1)
+      t1 = fma(trw[j], sr[j], t1);
+    else
+      t0 = fma(trw[j], sr[j], t0);
+  }
+  c.p = (p[0] + p[1]) + (p[2] + p[3]);
+  c.pt = quad_sum(t0 + t1);
+}
+
+/* One fused step K <= MP - 3 of both windows (hh_step_static's arithmetic, per half) */
+template <int K>
+__device__ __forceinline__ void h40_fstep(double (&A)[P40], const int (&M)[2], H40Carry &c, double2 (*s_vw)[P40],
+                                          double (*s_r)[P40 + 2], double (*s_d)[P40 + 4], double (*s_e)[P40],
+                                          double (*s_tau)[P40], double (*s_tail)[8][H40_TSTRIDE]) {
+  const int lane = css_lane_now();
+  const bool h = lane >= 32;
+  const int hi = h ? 1 : 0, r = lane & 31, tr = r >> 2, tq = lane & 3, R = H40_MAIN + tr;
+  const int mine = h ? M[1] : M[0];
+  const bool row = r < mine, trow = R < mine;
+  const double xi = (r > K + 1 && row) ? c.r : 0.0;
+  const double xr = (R > K + 1 && trow) ? c.rt : 0.0;
+  /* |x|^2 and r^T A r of each window in one half-wave sum; a tail row counts once */
+  double sigma = xi * xi + (tq == 0 ? xr * xr : 0.0);
+  double q = ((r > K && row) ? c.r * c.p : 0.0) + ((tq == 0 && R > K && trow) ? c.rt * c.pt : 0.0);
+  half_sum2(sigma, q);
+  double alpha, pr1, a11;
+  if constexpr (K + 1 < H40_MAIN) {
+    alpha = half_lane(c.r, K + 1, h);
+    pr1 = half_lane(c.p, K + 1, h);
+    a11 = half_lane(A[K + 1], K + 1, h);
+  } else {
+    alpha = half_lane(c.rt, 4 * (K + 1 - H40_MAIN), h);
+    pr1 = half_lane(c.pt, 4 * (K + 1 - H40_MAIN), h);
+    a11 = s_tail[hi][K + 1 - H40_MAIN][K + 1];
+  }
+  double tau, beta, scale, Kc;
+  hh_scalars(alpha, sigma, q, pr1, a11, &tau, &beta, &scale, &Kc);
+  const double ak1 = A[K + 1];
+  const double vi = (r == K + 1) ? 1.0 : xi * scale;
+  const double pi = (r > K && row) ? (tau * scale) * fma(-beta, ak1, c.p) : 0.0;
+  const double wi = fma(Kc, vi, pi);
+  const double akt = s_tail[hi][tr][K + 1];
+  const double vt = (R == K + 1) ? 1.0 : xr * scale;
+  const double ptl = (R > K && trow) ? (tau * scale) * fma(-beta, akt, c.pt) : 0.0;
+  const double wt = fma(Kc, vt, ptl);
+  double wk1;
+  if constexpr (K + 1 < H40_MAIN)
+    wk1 = half_lane(wi, K + 1, h);
+  else
+    wk1 = half_lane(wt, 4 * (K + 1 - H40_MAIN), h);
+  /* column K + 1 after this step (the update's formula at v_{K+1} = 1) */
+  const double rn = fma(-vi, wk1, fma(-wi, 1.0, ak1));
+  const double rnt = fma(-vt, wk1, fma(-wt, 1.0, akt));
+  __syncthreads();
+  if (r == 0) {
+    s_e[hi][K] = beta;
+    s_tau[hi][K] = tau;
+  }
+  s_vw[hi][r] = make_double2(vi, wi);
+  s_r[hi][r] = r > K + 1 ? rn : 0.0;
+  if (tq == 0) {
+    s_vw[hi][R] = make_double2(vt, wt);
+    s_r[hi][R] = R > K + 1 ? rnt : 0.0;
+  }
+  if constexpr (K + 1 < H40_MAIN) {
+    if (r == K + 1) s_d[hi][K + 1] = rn;
+  } else {
+    if (r == 4 * (K + 1 - H40_MAIN)) s_d[hi][K + 1] = rnt;
+  }
+  __syncthreads();
+  h40_fused_pass<K>(A, vi, wi, vt, wt, s_vw[hi], s_r[hi], s_tail[hi], c);
+  c.r = rn;
+  c.rt = rnt;
+}
+
+template <int K>
+struct H40FSteps {
+  static __device__ __forceinline__ void run(double (&A)[P40], const int (&M)[2], H40Carry &c, double2 (*s_vw)[P40],
+                                             double (*s_r)[P40 + 2], double (*s_d)[P40 + 4], double (*s_e)[P40],
+                                             double (*s_tau)[P40], double (*s_tail)[8][H40_TSTRIDE]) {
+    if ((K & 7) == 0 && K >= M[0] && K >= M[1]) return; /* exits only at block boundaries (hh_step_static) */
+    if constexpr (K <= P40 - 3) {
+      h40_fstep<K>(A, M, c, s_vw, s_r, s_d, s_e, s_tau, s_tail);
+      H40FSteps<K + 1>::run(A, M, c, s_vw, s_r, s_d, s_e, s_tau, s_tail);
+    } else {
+      /* K = MP - 2: no reflector; e_{MP-2} = column MP - 2 at row MP - 1, d_{MP-1} */
+      const int lane = css_lane_now();
+      const bool h = lane >= 32;
+      const int hi = h ? 1 : 0, r = lane & 31, mine = h ? M[1] : M[0];
+      const double e = half_lane(c.rt, 4 * (P40 - 1 - H40_MAIN), h);
+      __syncthreads();
+      if (r == 0) {
+        if (K == mine - 2) s_e[hi][K] = e;
+        s_d[hi][K + 1] = s_tail[hi][P40 - 1 - H40_MAIN][P40 - 1];
+      }
+    }
+  }
+};
 }  // namespace
 
 __global__ void __launch_bounds__(64, CSS_P40_WAVES)
@@ -3285,7 +3494,17 @@ __global__ void __launch_bounds__(64, CSS_P40_WAVES)
   CSS_PROF(1);
   /* ---- Householder tridiagonalisation of both windows (LAPACK dsytd2, lower) */
 #ifndef GD_CSS_SKIP_TRIDIAG
+#if CSS_H40_FUSED
+  {
+    /* (v_j, w_j) pairs over s_u.a.v / w (contiguous, 16-B aligned), column K + 1 over s_u.a.row */
+    double2(*s_vw)[MP] = reinterpret_cast<double2(*)[MP]>(&s_u.a.v[0][0]);
+    H40Carry cr;
+    h40_fused_start(A, s_u.a.row, s_d, s_tail, cr);
+    H40FSteps<0>::run(A, M, cr, s_vw, s_u.a.row, s_d, s_e, s_tau, s_tail);
+  }
+#else
   H40Steps<0>::run(A, M, s_u.a.row, s_u.a.v, s_u.a.w, s_d, s_e, s_tau, s_tail);
+#endif
 #endif
   __syncthreads();
 
