@@ -217,6 +217,27 @@ __device__ __forceinline__ void wave_sum2(double &a, double &b) {
   b = lane63(b);
 }
 
+/* all-reduce over each 16-lane DPP row (every stage combines a lane with its mirror image,
+ * so every lane of the row ends with the same bits) and over each 32-lane half (the two rows
+ * traded by v_permlane16_swap): VALU latency per stage instead of an LDS round trip per
+ * __shfl_xor */
+template <class Op>
+__device__ __forceinline__ double row_allreduce(double v) {
+  v = Op::op(v, dpp64<0xB1, 0xF>(v, 0.0));  /* quad_perm [1,0,3,2] */
+  v = Op::op(v, dpp64<0x4E, 0xF>(v, 0.0));  /* quad_perm [2,3,0,1] */
+  v = Op::op(v, dpp64<0x141, 0xF>(v, 0.0)); /* row_half_mirror */
+  return Op::op(v, dpp64<0x140, 0xF>(v, 0.0)); /* row_mirror */
+}
+template <class Op>
+__device__ __forceinline__ double half_allreduce(double v) {
+  v = row_allreduce<Op>(v);
+  const uint64_t u = __builtin_bit_cast(uint64_t, v);
+  const auto lo = __builtin_amdgcn_permlane16_swap((uint32_t)u, (uint32_t)u, false, false);
+  const auto hi = __builtin_amdgcn_permlane16_swap((uint32_t)(u >> 32), (uint32_t)(u >> 32), false, false);
+  return Op::op(__builtin_bit_cast(double, ((uint64_t)hi[0] << 32) | lo[0]),
+                __builtin_bit_cast(double, ((uint64_t)hi[1] << 32) | lo[1]));
+}
+
 /* block reductions over NW waves; red must hold 2*NW doubles */
 template <int NW, class Op>
 __device__ __forceinline__ double block_reduce(double v, double *red) {
@@ -375,12 +396,9 @@ __device__ __forceinline__ void bisect_top2(int m, double glo, double ghi, doubl
     }
     double nl = cnt <= target ? x : l;
     double nu = cnt <= target ? u : x;
-    /* half-wave max / min: xor butterflies inside each 32-lane half */
-#pragma unroll
-    for (int o = 16; o >= 1; o >>= 1) {
-      nl = fmax(nl, __shfl_xor(nl, o));
-      nu = fmin(nu, __shfl_xor(nu, o));
-    }
+    /* half-wave max / min */
+    nl = half_allreduce<OpMax>(nl);
+    nu = half_allreduce<OpMin>(nu);
     const bool same = (nl == l && nu == u);
     l = nl;
     u = nu;
@@ -2227,11 +2245,8 @@ __device__ __forceinline__ void p40_bisect(int mA, int mB, const double *glo, co
     }
     double nl = cnt <= target ? x : l;
     double nu = cnt <= target ? u : x;
-#pragma unroll
-    for (int o = 8; o >= 1; o >>= 1) {
-      nl = fmax(nl, __shfl_xor(nl, o));
-      nu = fmin(nu, __shfl_xor(nu, o));
-    }
+    nl = row_allreduce<OpMax>(nl); /* the quarter wave is one DPP row */
+    nu = row_allreduce<OpMin>(nu);
     if (!conv) {
       const bool same = (nl == l && nu == u);
       l = nl;

@@ -88,6 +88,9 @@ __device__ __forceinline__ double perm_xdist(const double *X, int i, int j) {
 #ifndef PERM_CHAINS
 #define PERM_CHAINS 1 /* composition chains per wave (1 or 2), see k_css_perm phase 2 */
 #endif
+#ifndef PERM_S16_PAIRS
+#define PERM_S16_PAIRS 1 /* the fp16 matrix from each unordered pair once (0: every entry) */
+#endif
 #ifndef PERM_MFMA
 #define PERM_MFMA 1 /* the permutation score on the matrix cores up to 80 individuals */
 #endif
@@ -950,6 +953,29 @@ __global__ void __launch_bounds__(PermShape<MP>::NT) PERM_WPE
       /* in FP32 (fp16 keeps 11 bits: the FP32 distance's ~2^-22 is inside the bound) */
       const float scf = (float)sc;
       constexpr int KC = SH::KT * 16;
+#if PERM_S16_PAIRS
+      /* zero the whole matrix (padding rows and columns, the diagonal), then every
+       * unordered pair once, written to both (x, y) and (y, x): S is symmetric bit for bit
+       * (dx and dy only change sign) */
+      for (int e = ln; e < SH::S16 / 16; e += NT) reinterpret_cast<uint4 *>(s_U)[e] = make_uint4(0u, 0u, 0u, 0u);
+      __syncthreads();
+      for (int e = ln; e < m * (m - 1) / 2; e += NT) {
+        /* pair e = T(h) + l, h > l: h from the float root of 8e + 1 (within one of the true
+         * row for e < 2^24), then corrected */
+        int h = (int)((1.0f + __fsqrt_rn(8.0f * (float)e + 1.0f)) * 0.5f);
+        if (h * (h - 1) / 2 > e)
+          --h;
+        else if (h * (h + 1) / 2 <= e)
+          ++h;
+        const int l = e - h * (h - 1) / 2;
+        const float dx = (float)(s_X[2 * h] - s_X[2 * l]), dy = (float)(s_X[2 * h + 1] - s_X[2 * l + 1]);
+        float v = __fsqrt_rn(dx * dx + dy * dy) * scf;
+        if (v < 0x1p-14f) v = 0.f; /* no fp16 denormals (score_mfma's SUB) */
+        const _Float16 hv = (_Float16)v;
+        *reinterpret_cast<_Float16 *>(s_U + h * SH::RS + 2 * l) = hv;
+        *reinterpret_cast<_Float16 *>(s_U + l * SH::RS + 2 * h) = hv;
+      }
+#else
       for (int e = ln; e < SH::MT * 32 * KC; e += NT) {
         const int row = e / KC, k = e - row * KC;
         float v = 0.f;
@@ -960,6 +986,7 @@ __global__ void __launch_bounds__(PermShape<MP>::NT) PERM_WPE
         }
         *reinterpret_cast<_Float16 *>(s_U + row * SH::RS + 2 * k) = (_Float16)v;
       }
+#endif
       PERM_PROF(6); /* the fp16 matrix */
       const gd_randint rb = perm_rd((uint32_t)(b > 1 ? b : 2), s_mag[b > 1 ? b : 2]);
       obs = score_exact_wave<MP>([](int k) { return (uint32_t)k; }, s_X, a, b, inva, invb, lane, my_lst, rb);
