@@ -169,16 +169,17 @@ def test_device_synth_matches_numpy():
         assert np.array_equal(x.cpu().numpy(), y)
 
 
-@pytest.mark.parametrize("groups", [None, "1", "2", "4", "2s", "4s"])
+@pytest.mark.parametrize("groups", [None, "1", "2", "4", "2g1", "3g2"])
 def test_device_batch_api_matches_host(oracle, monkeypatch, groups):
     """Several chromosomes in one device scan == per-chromosome scans; with GD_GROUPS the
     scan pipelines chromosome groups over the context's streams (the default, two groups,
     their window kernels on alternating streams, running concurrently; one group runs every
-    pass on the caller's stream); "s": GD_WALT=0, every window kernel on one stream."""
+    pass on the caller's stream); "<g>g<n>": g groups, the first of n chromosomes (GD_GROUP0)."""
     if groups:
-        monkeypatch.setenv("GD_GROUPS", groups.rstrip("s"))
-        if groups.endswith("s"):
-            monkeypatch.setenv("GD_WALT", "0")
+        g, _, n0 = groups.partition("g")
+        monkeypatch.setenv("GD_GROUPS", g)
+        if n0:
+            monkeypatch.setenv("GD_GROUP0", n0)
     import torch
     from gdscan import _lib, synth
     from gdscan._lib import Chrom, check, lib
