@@ -89,7 +89,7 @@ int64_t gd_css_big_grid(int64_t wtotal, int mp) {
     n = (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0) ? v : 256;
     if (dev < NDEV) cus[dev].store(n);
   }
-  int64_t grid = (int64_t)n * (mp <= 256 ? 4 : 2);
+  int64_t grid = (int64_t)n * (mp <= 256 ? 4 : mp <= 1024 ? 2 : 1); /* 2048 tier: one ~120 KB-LDS workgroup per CU */
   if (const char *e = getenv("GD_CSS_BIG_GRID")) {
     const long long g = atoll(e);
     if (g > 0) grid = g;
@@ -1095,7 +1095,9 @@ static int css_scan_locked(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, cons
     max_words = std::max(max_words, std::max(wa * d.asize, wb * d.bsize));
   }
   const int mp = gd_css_tier(mmax);
-  if (mp == 0) return fail(GD_ERR_SIZE, "asize + bsize above the largest supported cohort (GD_CSS_BIG_MAX = 1024)");
+  if (mp == 0) return fail(GD_ERR_SIZE, "asize + bsize above the largest supported cohort (GD_CSS_BIG_MAX = 2048)");
+  if (mds != 0 && mp > GD_CSS_SMACOF_MAX)
+    return fail(GD_ERR_SIZE, "SMACOF (mds 1 / 2) above the largest supported cohort (GD_CSS_SMACOF_MAX = 1024)");
   /* the general path (m above the register tiers): one matrix slab per workgroup */
   const int64_t slab_doubles = mp > GD_CSS_TIER_MAX ? gd_css_big_grid(pl.wtotal, mp) * gd_css_big_slab_per_wg(mp) : 1;
   if (drosophila)

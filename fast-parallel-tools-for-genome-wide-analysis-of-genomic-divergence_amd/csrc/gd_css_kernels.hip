@@ -3766,29 +3766,37 @@ __global__ void __launch_bounds__(MP / R)
                   double *pvals, double *xbuf, uint8_t *status, unsigned *flags, double *slab, int64_t slab_per_wg,
                   int ld) {
   constexpr int NT = MP / R, NW = NT / 64;
-  constexpr bool LUG = R > 1; /* inverse-iteration factors in the slab (LDS budget) */
+  constexpr bool LUG = R > 1;      /* inverse-iteration factors in the slab (LDS budget) */
+  constexpr bool GSL = MP > 1024;  /* the 2048 tier: masks, iterates and coordinates in the slab too */
+  static_assert(!LUG || MP == 1024 || MP == 2048, "the slab tail is sized for the 1024 and 2048 tiers");
+  constexpr int64_t LU_D = MP > 1024 ? GD_CSS_BIG_LU_DOUBLES_2K : GD_CSS_BIG_LU_DOUBLES;
+  constexpr int64_t GX_D = GSL ? GD_CSS_BIG_GX_DOUBLES_2K : 0;
   __shared__ double s_row[MP + 2];
   __shared__ double s_v[MP], s_w[MP];
   __shared__ __attribute__((aligned(16))) double s_d[MP + 4];
   __shared__ __attribute__((aligned(16))) double s_e2[MP + 4];
   __shared__ double s_e[MP], s_tau[MP];
-  __shared__ uint64_t s_mask[2 * MP];
-  __shared__ double s_y[2][MP];
+  __shared__ uint64_t s_mask_l[GSL ? 1 : 2 * MP];
+  __shared__ double s_y_l[2][GSL ? 1 : MP];
   __shared__ double s_lu_l[2][3][LUG ? 1 : MP];
   __shared__ uint8_t s_piv_l[2][LUG ? 1 : MP];
-  __shared__ double s_x[2 * MP];
+  __shared__ double s_x_l[GSL ? 1 : 2 * MP];
   __shared__ int s_tr[MP];
   __shared__ double s_lam[2];
   __shared__ double s_red[2 * (2 * NW + 2)];
 
   const int tid = threadIdx.x;
   double *A = slab + (int64_t)blockIdx.x * slab_per_wg;
-  static_assert(!LUG || MP == 1024, "GD_CSS_BIG_LU_DOUBLES is sized for the 1024 tier");
-  double *lug = A + slab_per_wg - GD_CSS_BIG_LU_DOUBLES; /* the slab's tail (gd_css_big_slab_per_wg) */
+  /* the slab's tail (gd_css_big_slab_per_wg): the factors, then (2048 tier) the vectors */
+  double *lug = A + slab_per_wg - (LUG ? LU_D : 0) - GX_D;
+  double *gx = A + slab_per_wg - GX_D;
   double(*s_lu)[3][MP] = LUG ? reinterpret_cast<double(*)[3][MP]>(lug)
                              : reinterpret_cast<double(*)[3][MP]>(&s_lu_l[0][0][0]);
   uint8_t(*s_piv)[MP] = LUG ? reinterpret_cast<uint8_t(*)[MP]>(lug + 6 * MP)
                             : reinterpret_cast<uint8_t(*)[MP]>(&s_piv_l[0][0]);
+  uint64_t *s_mask = GSL ? reinterpret_cast<uint64_t *>(gx) : &s_mask_l[0];
+  double(*s_y)[MP] = GSL ? reinterpret_cast<double(*)[MP]>(gx + 2 * MP) : reinterpret_cast<double(*)[MP]>(&s_y_l[0][0]);
+  double *s_x = GSL ? gx + 4 * MP : &s_x_l[0];
   auto at = [&](int r, int c) -> double & { return A[(int64_t)c * ld + r]; };
   for (int t = tid; t < MP; t += NT) s_tr[t] = t;
 
@@ -4224,8 +4232,10 @@ static int launch_big(int mp, const gd_chrom_dev *d_ch, int nchrom, const gd_css
     CSS_BIG(256, 1);
   else if (mp <= 512)
     CSS_BIG(512, 1);
-  else
+  else if (mp <= 1024)
     CSS_BIG(1024, 2);
+  else
+    CSS_BIG(2048, 4);
 #undef CSS_BIG
   return hipGetLastError() == hipSuccess ? GD_OK : GD_ERR_HIP;
 }

@@ -1294,9 +1294,9 @@ __global__ void __launch_bounds__(PermShape<MP>::NT) PERM_WPE
 /* observed score is the same function of the identity tracks.                    */
 /* ------------------------------------------------------------------------ */
 namespace {
-/* permutations per pass: 64, 32 at the 1024 tier (its byte-pair matrix is MP x P u16) */
+/* permutations per pass: 64, 32 at the 1024 tier, 16 at 2048 (the u16 matrix is MP x P) */
 template <int MP>
-constexpr int pb_p() { return MP > 512 ? 32 : 64; }
+constexpr int pb_p() { return MP > 1024 ? 16 : MP > 512 ? 32 : 64; }
 
 /* Fisher-Yates of random_shuffle (css.c:700-706) on column `col` (stride PB_P), draws
  * from state x without rejection; true if a draw would have been rejected */
@@ -1583,8 +1583,11 @@ int gd_css_perm_launch(int mp, const gd_chrom_dev *d_ch, int nchrom, const doubl
     else if (mp <= 512)
       hipLaunchKernelGGL(k_css_perm_big<512>, dim3(grid), dim3(256), 0, s, d_ch, nchrom, xbuf, 2 * mp, status, wtotal,
                          treshold, runs, p, wq, slab, per, ld);
-    else
+    else if (mp <= 1024)
       hipLaunchKernelGGL(k_css_perm_big<1024>, dim3(grid), dim3(256), 0, s, d_ch, nchrom, xbuf, 2 * mp, status,
+                         wtotal, treshold, runs, p, wq, slab, per, ld);
+    else
+      hipLaunchKernelGGL(k_css_perm_big<2048>, dim3(grid), dim3(256), 0, s, d_ch, nchrom, xbuf, 2 * mp, status,
                          wtotal, treshold, runs, p, wq, slab, per, ld);
     return hipGetLastError() == hipSuccess ? GD_OK : GD_ERR_HIP;
   }

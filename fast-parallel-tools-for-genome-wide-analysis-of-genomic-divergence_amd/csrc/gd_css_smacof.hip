@@ -526,7 +526,7 @@ int gd_css_smacof_launch(int mp, bool freq, const gd_chrom_dev *d_ch, int nchrom
       if (mp > 256 && mp <= 512)
         return launch_smacof<512, false, true>(d_ch, nchrom, d_pl, planes, lo_a, hi_a, lo_b, avals, bvals, wtotal, mds,
                                                want_x, force_literal, xs, scores, p, xbuf, status, flags, s, slab, mp);
-      if (mp > 512 && mp <= GD_CSS_BIG_MAX)
+      if (mp > 512 && mp <= GD_CSS_SMACOF_MAX)
         return launch_smacof<1024, false, true>(d_ch, nchrom, d_pl, planes, lo_a, hi_a, lo_b, avals, bvals, wtotal,
                                                 mds, want_x, force_literal, xs, scores, p, xbuf, status, flags, s, slab,
                                                 mp);

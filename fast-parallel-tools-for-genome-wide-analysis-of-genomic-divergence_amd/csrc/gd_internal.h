@@ -38,20 +38,29 @@ typedef struct gd_chrom_dev {
 #define GD_NREP 100 /* bootstrap replicates (cFisher.c:62) */
 
 /* CSS cohort sizes (m = asize + bsize): register tiers up to GD_CSS_TIER_MAX; the general
- * path (k_css_mds_big, k_css_perm_big, k_css_smacof_big) above, up to GD_CSS_BIG_MAX, with
- * each workgroup's matrices in a global-memory slab of its own */
+ * path (k_css_mds_big, k_css_perm_big, k_css_smacof_big) above, up to GD_CSS_BIG_MAX (SMACOF,
+ * mds 1 / 2: up to GD_CSS_SMACOF_MAX, one thread per individual), with each workgroup's
+ * matrices in a global-memory slab of its own */
 #define GD_CSS_TIER_MAX 128
-#define GD_CSS_BIG_MAX 1024
+#define GD_CSS_BIG_MAX 2048
+#define GD_CSS_SMACOF_MAX 1024
 /* doubles at the end of a 1024-tier slab for the inverse-iteration factors (LDS budget) */
 #define GD_CSS_BIG_LU_DOUBLES (6 * 1024 + 2 * 1024 / 8 + 8)
+/* the 2048 tier's: the factors, then its vectors that leave LDS (the 64-SNP compare masks,
+ * the two eigenvector iterates and the multipliers / coordinates, 2 m each) */
+#define GD_CSS_BIG_LU_DOUBLES_2K (6 * 2048 + 2 * 2048 / 8 + 8)
+#define GD_CSS_BIG_GX_DOUBLES_2K (6 * 2048)
+static inline int64_t gd_css_big_tail_doubles(int m) {
+  return m > 1024 ? GD_CSS_BIG_LU_DOUBLES_2K + GD_CSS_BIG_GX_DOUBLES_2K : m > 512 ? GD_CSS_BIG_LU_DOUBLES : 0;
+}
 /* leading dimension (doubles) of a general-path matrix: m rounded up to 128-byte columns */
 static inline int gd_css_big_ld(int m) { return (m + 15) & ~15; }
 /* doubles of one workgroup's slab: the m x ld matrix of the MDS / permutation kernels or
- * SMACOF's 16-bit counts + packed stress triangle, whichever is larger */
+ * SMACOF's 16-bit counts + packed stress triangle, whichever is larger, and the tier's tail */
 static inline int64_t gd_css_big_slab_per_wg(int m) {
   const int64_t mds = (int64_t)gd_css_big_ld(m) * m;
   const int64_t sm = (int64_t)m * (m - 1) / 2 + 8 + ((int64_t)gd_css_big_ld(m) * m + 3) / 4 + 8;
-  return (mds > sm ? mds : sm) + 32 + (m > 512 ? GD_CSS_BIG_LU_DOUBLES : 0);
+  return (mds > sm ? mds : sm) + 32 + gd_css_big_tail_doubles(m);
 }
 /* Workgroups (= slabs) of the general-path kernels for a batch of wtotal windows and tier
  * mp: the device's resident capacity -- CUs x 4 workgroups of the 256-thread tier, x 2 of

@@ -1,9 +1,9 @@
-"""GPU: the general CSS path for cohorts above the register tiers (128 < m <= 1024;
+"""GPU: the general CSS path for cohorts above the register tiers (128 < m <= 2048;
 k_css_mds_big, k_css_perm_big, k_css_smacof<.., BIG>), which the reference supports for
 any m (threadcss.c:191,207-215; css.c:181-223).  Scores against the oracle at 1e-9
 relative; permutation p on the device's own coordinates inside the oracle's near-tie
 bracket (as tests/test_css_perm_isolated.py); SMACOF (mds 1) against the oracle's
-reference-order restatement; cohorts above 1024 refused.  The serial window set keeps
+reference-order restatement (SMACOF up to 1024); cohorts above 2048 refused.  The serial window set keeps
 the oracle's O(m^3) per-window cost to seconds."""
 import numpy as np
 import pytest
@@ -75,10 +75,14 @@ def test_general_path_smacof(opt):
 
 
 def test_above_the_general_path_raises():
+    """above 2048 individuals (and SMACOF above 1024) a scan returns GD_ERR_SIZE"""
     from gdscan import GdError, css, synth
-    av, bv, ap, bp, regend = synth.chromosome(240, 60, 520, 520)
+    av, bv, ap, bp, regend = synth.chromosome(240, 60, 1030, 1030)
     with pytest.raises(GdError):
         css.scan(av, bv, ap, bp, regend, serial=True)
+    av, bv, ap, bp, regend = synth.chromosome(241, 60, 520, 520)
+    with pytest.raises(GdError):
+        css.scan(av, bv, ap, bp, regend, runs=0, mds=1, serial=True)
 
 
 def _lapack_scores(orc, av, bv, ap, bp, regend, a, b, wsize=2500, wstep=500):
@@ -119,10 +123,14 @@ def _lapack_scores(orc, av, bv, ap, bp, regend, a, b, wsize=2500, wstep=500):
     return out
 
 
-@pytest.mark.parametrize("a,b,nsnp,runs", [(300, 300, 150, 30), (700, 290, 110, 0), (512, 512, 100, 0)])
+@pytest.mark.parametrize("a,b,nsnp,runs", [(300, 300, 150, 30), (700, 290, 110, 0), (512, 512, 100, 0),
+                                            # the 2048 tier (1025..2048: four rows per thread, the masks,
+                                            # iterates and coordinates in the slab, 16 permutations per pass)
+                                            (520, 520, 100, 20), (1000, 700, 90, 0)])
 def test_cohorts_above_512(oracle, a, b, nsnp, runs):
     """The 1024 tier (513..1024 individuals: two rows per thread in k_css_mds_big, the
-    inverse-iteration factors in the slab, 32 permutations per pass in k_css_perm_big):
+    inverse-iteration factors in the slab, 32 permutations per pass in k_css_perm_big) and
+    the 2048 tier:
     scores against the LAPACK-eigen-step restatement at 1e-9, permutation p on the
     device's own coordinates inside the oracle's tie bracket.  The reference scores any
     m (threadcss.c:191,207-215; css.c:181-223)."""
