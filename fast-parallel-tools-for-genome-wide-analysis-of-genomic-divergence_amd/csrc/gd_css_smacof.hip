@@ -199,14 +199,17 @@ __global__ void __launch_bounds__(256)
  * live in the workgroup's global-memory slab (tri first, mpb (mpb - 1) / 2 doubles for the
  * batch's tier mpb, then the counts at column stride ld) and the workgroups loop over
  * windows; otherwise both are in LDS, one workgroup per window. */
+/* threads of a tier: one per individual up to 1024, two individuals per thread above */
+template <int MP>
+constexpr int sm_nt() { return MP > 1024 ? 1024 : 64 * ((MP + 63) / 64); }
 template <int MP, bool FREQ, bool BIG>
-__global__ void __launch_bounds__(64 * ((MP + 63) / 64))
+__global__ void __launch_bounds__(sm_nt<MP>())
     k_css_smacof(const gd_chrom_dev *ch, int nchrom, const gd_css_planes *pl, const uint32_t *planes,
                  const int32_t *lo_a_, const int32_t *hi_a_, const int32_t *lo_b_, const double *avals,
                  const double *bvals, int64_t wtotal, int mds, int want_x, int force_literal, int xstride,
                  double *scores, double *pvals, double *xbuf, uint8_t *status, unsigned *flags, double *slab,
                  int64_t slab_per_wg, int mpb, int ld) {
-  constexpr int NT = 64 * ((MP + 63) / 64), NW = NT / 64;
+  constexpr int NT = sm_nt<MP>(), NW = NT / 64, SR = (MP + NT - 1) / NT; /* SR individuals per thread */
   constexpr int NTRI = MP * (MP - 1) / 2;
   __shared__ uint16_t s_cnt_l[BIG ? 1 : MP * MP]; /* count D[i][j] at j*cs + i */
   __shared__ double s_tri_l[BIG ? 1 : NTRI];      /* stress terms, (i, j < i) at i(i-1)/2 + j */
@@ -241,7 +244,9 @@ __global__ void __launch_bounds__(64 * ((MP + 63) / 64))
     if (tid == 0) atomicOr(flags, GD_FLAG_BAD_SIZE);
     continue;
   }
-  const bool row = tid < m;
+  /* individual i = tid + rr NT of this thread, rr < SR */
+#define SM_ROWS(i) \
+  _Pragma("unroll") for (int rr_ = 0, i = tid; rr_ < SR; ++rr_, i += NT) if (i < m)
 
   /* ---- dissimilarities + fill_averages */
   double avg = 0.0, fdel = 0.0;
@@ -281,19 +286,19 @@ __global__ void __launch_bounds__(64 * ((MP + 63) / 64))
         const int nb = min(64, npos - 64 * k);
         const uint64_t tail = nb == 64 ? ~0ull : ((1ull << nb) - 1);
         __syncthreads();
-        if (row) {
-          const uint32_t *base = tid < a ? pa + (int64_t)(2 * tid) * P.wa : pb + (int64_t)(2 * (tid - a)) * P.wb;
-          const int64_t nw = tid < a ? P.wa : P.wb;
-          const int64_t r = (tid < a ? ra : rb) + 64 * k;
-          s_mask[2 * tid] = sm_plane_bits64(base, r) & tail;
-          s_mask[2 * tid + 1] = sm_plane_bits64(base + nw, r) & tail;
+        SM_ROWS(i) {
+          const uint32_t *base = i < a ? pa + (int64_t)(2 * i) * P.wa : pb + (int64_t)(2 * (i - a)) * P.wb;
+          const int64_t nw = i < a ? P.wa : P.wb;
+          const int64_t r = (i < a ? ra : rb) + 64 * k;
+          s_mask[2 * i] = sm_plane_bits64(base, r) & tail;
+          s_mask[2 * i + 1] = sm_plane_bits64(base + nw, r) & tail;
         }
         __syncthreads();
-        if (row) {
-          const uint64_t Pi = s_mask[2 * tid], Ni = s_mask[2 * tid + 1];
+        SM_ROWS(i) {
+          const uint64_t Pi = s_mask[2 * i], Ni = s_mask[2 * i + 1];
           for (int j = 0; j < m; ++j) {
             const uint64_t Pj = s_mask[2 * j], Nj = s_mask[2 * j + 1];
-            s_cnt[j * cs + tid] = (uint16_t)(s_cnt[j * cs + tid] + __popcll(Pi & Nj) + __popcll(Ni & Pj));
+            s_cnt[j * cs + i] = (uint16_t)(s_cnt[j * cs + i] + __popcll(Pi & Nj) + __popcll(Ni & Pj));
           }
         }
       }
@@ -301,18 +306,18 @@ __global__ void __launch_bounds__(64 * ((MP + 63) / 64))
       const double *av = avals + d.a_off + la, *bv = bvals + d.b_off + lb;
       for (int k = 0; k < npos; ++k) {
         __syncthreads();
-        if (row) s_vals[tid] = tid < a ? av[(int64_t)k * a + tid] : bv[(int64_t)k * b + (tid - a)];
+        SM_ROWS(i) s_vals[i] = i < a ? av[(int64_t)k * a + i] : bv[(int64_t)k * b + (i - a)];
         __syncthreads();
-        if (row) {
-          const double vi = s_vals[tid];
+        SM_ROWS(i) {
+          const double vi = s_vals[i];
           for (int j = 0; j < m; ++j) {
-            if (j == tid) continue; /* (int)v * v >= 0 never counts */
+            if (j == i) continue; /* (int)v * v >= 0 never counts */
             const double vj = s_vals[j];
             /* the reference casts the row element of the larger index within a population
              * and the A element across populations (css.c:281-326) */
-            const bool cast_i = ((tid < a) == (j < a)) ? (tid > j) : (tid < a);
+            const bool cast_i = ((i < a) == (j < a)) ? (i > j) : (i < a);
             const double prod = cast_i ? sm_x86_int(vi) * vj : sm_x86_int(vj) * vi;
-            if (prod == -9.0) s_cnt[j * cs + tid] = (uint16_t)(s_cnt[j * cs + tid] + 1);
+            if (prod == -9.0) s_cnt[j * cs + i] = (uint16_t)(s_cnt[j * cs + i] + 1);
           }
         }
       }
@@ -320,14 +325,15 @@ __global__ void __launch_bounds__(64 * ((MP + 63) / 64))
     __syncthreads();
     /* fill_averages (css.c:337-366): zero counts, the diagonal included, are unknown */
     double unv = 0.0, sum = 0.0;
-    if (row)
+    SM_ROWS(i) {
       for (int j = 0; j < m; ++j) {
-        const int cj = s_cnt[j * cs + tid];
+        const int cj = s_cnt[j * cs + i];
         if (cj == 0)
           unv += 1.0;
         else
           sum += (double)cj;
       }
+    }
     /* sums of integers: exact in any order */
     for (int o = 32; o > 0; o >>= 1) {
       unv += __shfl_xor(unv, o);
@@ -365,17 +371,17 @@ __global__ void __launch_bounds__(64 * ((MP + 63) / 64))
   auto pass = [&](int cur) -> double {
     const double *Z = s_z[cur];
     double *Xn = s_z[cur ^ 1];
-    if (row) {
-      const double zi0 = Z[2 * tid], zi1 = Z[2 * tid + 1];
-      const int tb = tid * (tid - 1) / 2;
+    SM_ROWS(i) {
+      const double zi0 = Z[2 * i], zi1 = Z[2 * i + 1];
+      const int tb = i * (i - 1) / 2;
       double dsum = 0.0;
       for (int j = m - 1; j >= 0; --j) {
-        if (j == tid) continue;
+        if (j == i) continue;
         const double dij = sm_dist(zi0, zi1, Z[2 * j], Z[2 * j + 1]);
-        const double del = delta(tid, j);
+        const double del = delta(i, j);
         const double bij = dij < 0.00001 ? 0.0 : -1 * del / dij;
         dsum += bij;
-        if (j < tid) {
+        if (j < i) {
           const double e = dij - del;
           s_tri[tb + j] = e * e;
         }
@@ -383,19 +389,19 @@ __global__ void __launch_bounds__(64 * ((MP + 63) / 64))
       double x0 = 0.0, x1 = 0.0;
       for (int k = 0; k < m; ++k) {
         double bik;
-        if (k == tid) {
+        if (k == i) {
           bik = -1 * dsum;
         } else {
           const double dik = sm_dist(zi0, zi1, Z[2 * k], Z[2 * k + 1]);
-          bik = dik < 0.00001 ? 0.0 : -1 * delta(tid, k) / dik;
+          bik = dik < 0.00001 ? 0.0 : -1 * delta(i, k) / dik;
         }
         if (bik != 0.0) {
           x0 = x0 + bik * Z[2 * k];
           x1 = x1 + bik * Z[2 * k + 1];
         }
       }
-      Xn[2 * tid] = x0 / m;
-      Xn[2 * tid + 1] = x1 / m;
+      Xn[2 * i] = x0 / m;
+      Xn[2 * i + 1] = x1 / m;
     }
     __syncthreads();
     if (tid == 0) {
@@ -424,9 +430,9 @@ __global__ void __launch_bounds__(64 * ((MP + 63) / 64))
 
   const double *Xf;
   if (mds == 2) {
-    if (row) {
-      s_z[0][2 * tid] = xbuf[w * xstride + 2 * tid];
-      s_z[0][2 * tid + 1] = xbuf[w * xstride + 2 * tid + 1];
+    SM_ROWS(i) {
+      s_z[0][2 * i] = xbuf[w * xstride + 2 * i];
+      s_z[0][2 * i + 1] = xbuf[w * xstride + 2 * i + 1];
     }
     __syncthreads();
     int fin;
@@ -439,19 +445,19 @@ __global__ void __launch_bounds__(64 * ((MP + 63) / 64))
     bool have = false;
     for (int r = 0; r < SM_NINIT; ++r) {
       __syncthreads();
-      if (row) {
-        const uint64_t k = (uint64_t)r * 2 * m + 2 * tid; /* draws before this lane's two */
-        s_z[0][2 * tid] = sm_drand48_at(x0, k + 1);
-        s_z[0][2 * tid + 1] = sm_drand48_at(x0, k + 2);
+      SM_ROWS(i) {
+        const uint64_t k = (uint64_t)r * 2 * m + 2 * i; /* draws before this individual's two */
+        s_z[0][2 * i] = sm_drand48_at(x0, k + 1);
+        s_z[0][2 * i + 1] = sm_drand48_at(x0, k + 2);
       }
       __syncthreads();
       int fin;
       const double sigma = smacof(&fin);
       const bool take = sigma < best || (!have && (r == 0 || sigma < fallback));
       if (take) {
-        if (row) {
-          s_best[2 * tid] = s_z[fin][2 * tid];
-          s_best[2 * tid + 1] = s_z[fin][2 * tid + 1];
+        SM_ROWS(i) {
+          s_best[2 * i] = s_z[fin][2 * i];
+          s_best[2 * i + 1] = s_z[fin][2 * i + 1];
         }
         if (sigma < best) {
           best = sigma;
@@ -484,6 +490,8 @@ __global__ void __launch_bounds__(64 * ((MP + 63) / 64))
   }
 }
 
+#undef SM_ROWS
+
 template <int MP, bool FREQ, bool BIG = false>
 static int launch_smacof(const gd_chrom_dev *d_ch, int nchrom, const gd_css_planes *d_pl, const uint32_t *planes,
                          const int32_t *lo_a, const int32_t *hi_a, const int32_t *lo_b, const double *avals,
@@ -491,7 +499,7 @@ static int launch_smacof(const gd_chrom_dev *d_ch, int nchrom, const gd_css_plan
                          double *scores, double *p, double *xbuf, uint8_t *status, unsigned *flags, hipStream_t s,
                          double *slab = nullptr, int mpb = 0) {
   const int64_t grid = BIG ? gd_css_big_grid(wtotal, mpb) : wtotal;
-  hipLaunchKernelGGL((k_css_smacof<MP, FREQ, BIG>), dim3((unsigned)grid), dim3(64 * ((MP + 63) / 64)), 0, s, d_ch,
+  hipLaunchKernelGGL((k_css_smacof<MP, FREQ, BIG>), dim3((unsigned)grid), dim3(sm_nt<MP>()), 0, s, d_ch,
                      nchrom, d_pl, planes, lo_a, hi_a, lo_b, avals, bvals, wtotal, mds, want_x, force_literal,
                      xstride, scores, p, xbuf, status, flags, slab, BIG ? gd_css_big_slab_per_wg(mpb) : 0, mpb,
                      BIG ? gd_css_big_ld(mpb) : 0);
@@ -526,8 +534,12 @@ int gd_css_smacof_launch(int mp, bool freq, const gd_chrom_dev *d_ch, int nchrom
       if (mp > 256 && mp <= 512)
         return launch_smacof<512, false, true>(d_ch, nchrom, d_pl, planes, lo_a, hi_a, lo_b, avals, bvals, wtotal, mds,
                                                want_x, force_literal, xs, scores, p, xbuf, status, flags, s, slab, mp);
-      if (mp > 512 && mp <= GD_CSS_SMACOF_MAX)
+      if (mp > 512 && mp <= 1024)
         return launch_smacof<1024, false, true>(d_ch, nchrom, d_pl, planes, lo_a, hi_a, lo_b, avals, bvals, wtotal,
+                                                mds, want_x, force_literal, xs, scores, p, xbuf, status, flags, s, slab,
+                                                mp);
+      if (mp > 1024 && mp <= GD_CSS_SMACOF_MAX)
+        return launch_smacof<2048, false, true>(d_ch, nchrom, d_pl, planes, lo_a, hi_a, lo_b, avals, bvals, wtotal,
                                                 mds, want_x, force_literal, xs, scores, p, xbuf, status, flags, s, slab,
                                                 mp);
   }

@@ -39,11 +39,11 @@ typedef struct gd_chrom_dev {
 
 /* CSS cohort sizes (m = asize + bsize): register tiers up to GD_CSS_TIER_MAX; the general
  * path (k_css_mds_big, k_css_perm_big, k_css_smacof_big) above, up to GD_CSS_BIG_MAX (SMACOF,
- * mds 1 / 2: up to GD_CSS_SMACOF_MAX, one thread per individual), with each workgroup's
- * matrices in a global-memory slab of its own */
+ * mds 1 / 2: up to GD_CSS_SMACOF_MAX, two individuals per thread above 1024), with each
+ * workgroup's matrices in a global-memory slab of its own */
 #define GD_CSS_TIER_MAX 128
 #define GD_CSS_BIG_MAX 2048
-#define GD_CSS_SMACOF_MAX 1024
+#define GD_CSS_SMACOF_MAX 2048
 /* doubles at the end of a 1024-tier slab for the inverse-iteration factors (LDS budget) */
 #define GD_CSS_BIG_LU_DOUBLES (6 * 1024 + 2 * 1024 / 8 + 8)
 /* the 2048 tier's: the factors, then its vectors that leave LDS (the 64-SNP compare masks,

@@ -75,14 +75,12 @@ def test_general_path_smacof(opt):
 
 
 def test_above_the_general_path_raises():
-    """above 2048 individuals (and SMACOF above 1024) a scan returns GD_ERR_SIZE"""
+    """above 2048 individuals a scan returns GD_ERR_SIZE, classical or SMACOF"""
     from gdscan import GdError, css, synth
     av, bv, ap, bp, regend = synth.chromosome(240, 60, 1030, 1030)
-    with pytest.raises(GdError):
-        css.scan(av, bv, ap, bp, regend, serial=True)
-    av, bv, ap, bp, regend = synth.chromosome(241, 60, 520, 520)
-    with pytest.raises(GdError):
-        css.scan(av, bv, ap, bp, regend, runs=0, mds=1, serial=True)
+    for mds in (0, 1):
+        with pytest.raises(GdError):
+            css.scan(av, bv, ap, bp, regend, runs=0, mds=mds, serial=True)
 
 
 def _lapack_scores(orc, av, bv, ap, bp, regend, a, b, wsize=2500, wstep=500):
@@ -178,11 +176,13 @@ def test_general_path_several_windows_per_workgroup(oracle, opt, monkeypatch):
     assert _close_frac(s1, s1_ref, 1e-9) == 1.0
 
 
-def test_cohorts_above_512_smacof(opt):
+@pytest.mark.parametrize("a,b,nsnp", [(300, 300, 100), (520, 520, 100)])
+def test_cohorts_above_512_smacof(opt, a, b, nsnp):
     """SMACOF (mds 1) at the 1024 tier (1024-thread workgroups, counts and stress triangle
-    in the slab) against the oracle's reference-order restatement."""
+    in the slab) and the 2048 tier (two individuals per thread) against the oracle's
+    reference-order restatement."""
     from gdscan import css, synth
-    av, bv, ap, bp, regend = synth.chromosome(275, 100, 300, 300)
+    av, bv, ap, bp, regend = synth.chromosome(275 + a - 300, nsnp, a, b)
     s, _ = css.scan(av, bv, ap, bp, regend, runs=0, mds=1, seed=11, serial=True)
     s_ref, _ = oracle_scan_ex(opt, av, bv, ap, bp, regend, 0, 1, seed=11, serial=True)
     assert np.array_equal(s == 0, s_ref == 0) and (s_ref != 0).sum() >= 5
