@@ -88,6 +88,16 @@ __device__ __forceinline__ double perm_xdist(const double *X, int i, int j) {
 #ifndef PERM_CHAINS
 #define PERM_CHAINS 1 /* composition chains per wave (1 or 2), see k_css_perm phase 2 */
 #endif
+/* Diagnostics builds for per-phase counters (tools/perm_phase_pmc.sh; outputs are wrong in
+ * them): PERM_DIAG_NOEXIT runs every window's full mcR permutations (no early exit, so every
+ * build does the same passes); PERM_DIAG_SKIP bit 1 skips the Fisher-Yates draws (the
+ * identity permutations stay), bit 2 the compositions, bit 4 the scores (no hits). */
+#ifndef PERM_DIAG_NOEXIT
+#define PERM_DIAG_NOEXIT 0
+#endif
+#ifndef PERM_DIAG_SKIP
+#define PERM_DIAG_SKIP 0
+#endif
 #ifndef PERM_S16_PAIRS
 #define PERM_S16_PAIRS 1 /* the fp16 matrix from each unordered pair once (0: every entry) */
 #endif
@@ -1079,7 +1089,9 @@ __global__ void __launch_bounds__(PermShape<MP>::NT) PERM_WPE
       int lq = lane;
       PERM_OPAQUE(lq);
       uint8_t *col = my_sig + lq;
-#if PERM_FY_UNROLL
+#if PERM_DIAG_SKIP & 1
+      const bool rej = false;
+#elif PERM_FY_UNROLL
       /* (not at 64: the straight line raised that tier's VGPRs 160 -> 196, 3 -> 2 waves per SIMD) */
       const bool rej = (MP != 64 && m == MP) ? fy_fast_unrolled<MP>(col, gd_affine_apply(Jq, base))
                                              : fy_fast(col, gd_affine_apply(Jq, base), m, vm0, vm1);
@@ -1119,7 +1131,7 @@ __global__ void __launch_bounds__(PermShape<MP>::NT) PERM_WPE
        * read through the map s_fs[v]; with PERM_CHAINS == 2 every chain starts from the
        * identity and every lane reads through its chain's map (Fs_0 = the carried tracks),
        * which halves the chain of dependent ds_bpermutes */
-      {
+      if (!(PERM_DIAG_SKIP & 2)) {
         constexpr int CH = PERM_CHAINS, TL = 64 / CH;
         uint32_t pf0[16], pf1[16];
         int li = lane;
@@ -1183,7 +1195,7 @@ __global__ void __launch_bounds__(PermShape<MP>::NT) PERM_WPE
        * the previous one wrote).  PERM_CHAINS == 1: Fs_1 = F_63, Fs_v = Fs_{v-1} o G^{v-1}_63;
        * PERM_CHAINS == 2: Fs_0 = the carried tracks, Fs_u = Fs_{u-1} o G^{u-1}_end.  The carry
        * into the next pass is the last map composed with the last chain's end. */
-      if (wave == 0) {
+      if (!(PERM_DIAG_SKIP & 2) && wave == 0) {
         constexpr int NCH = NWV * PERM_CHAINS, U0 = PERM_CHAINS == 1 ? 1 : 0;
         for (int u = U0; u < NCH; ++u) {
           for (int i = lane; i < m; i += 64)
@@ -1206,9 +1218,12 @@ __global__ void __launch_bounds__(PermShape<MP>::NT) PERM_WPE
       uint8_t *mcol = my_mem + lc;
       double est, err;
       /* the lane's chain map (PERM_CHAINS == 1: wave-uniform, none for wave 0) */
-      const bool mapped = PERM_CHAINS > 1 || __builtin_amdgcn_readfirstlane(wave) > 0;
+      const bool mapped = !(PERM_DIAG_SKIP & 2) && (PERM_CHAINS > 1 || __builtin_amdgcn_readfirstlane(wave) > 0);
       const uint8_t *fmap = s_fs + (PERM_CHAINS * wave + lc / (64 / PERM_CHAINS)) * MP;
-      if constexpr (SH::MF) {
+      if constexpr ((PERM_DIAG_SKIP & 4) != 0) {
+        est = -1e300; /* no hits */
+        err = 0.0;
+      } else if constexpr (SH::MF) {
         score_mfma<MP>(s16, s_lut, tcol, fmap, mapped, a, b, inva, invb, inv_sc, lane, est, err);
       } else {
         score_f32<MP>(s_S32, s_R, tcol, fmap, mapped, mcol, a, b, inva, invb, est, err);
@@ -1263,7 +1278,7 @@ __global__ void __launch_bounds__(PermShape<MP>::NT) PERM_WPE
         const uint64_t Hv = s_hit[v];
         const int vv = min(64, max(0, valid - 64 * v)); /* valid permutations of wave v */
         const int need = treshold - hits;
-        if (__popcll(Hv) >= need) {
+        if (!PERM_DIAG_NOEXIT && __popcll(Hv) >= need) {
           uint64_t h = Hv;
           for (int k = 1; k < need; ++k) h &= h - 1;
           nsc += __ffsll((unsigned long long)h); /* position of the need-th hit, + 1 */
