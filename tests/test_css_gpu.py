@@ -78,7 +78,7 @@ def test_irregular_values_take_the_literal_path(oracle, asize, bsize, nsnp, nbad
     """Values outside {3,0,-3,-10000} (including NaN and huge values) follow the
     reference predicate (int)v_i * v_j == -9 with x86 cast semantics.  With few bad
     values most windows stay on the popcount build, so literal and popcount windows
-    share the two-window waves of the p40 tier."""
+    share the two-window waves of the 40 tier."""
     from gdscan import css
     av, bv, ap, bp, regend = _synth(6, nsnp, asize, bsize)
     rng = np.random.default_rng(0)
@@ -157,7 +157,7 @@ def test_device_batch_api_matches_host(oracle):
 
 
 @pytest.mark.parametrize("shapes", [
-    # p40 tier: different (a, b) splits and m inside one two-window wave at every
+    # 40 tier: different (a, b) splits and m inside one two-window wave at every
     # chromosome boundary; odd per-chromosome window counts shift the pairing, and the
     # batch's total is odd (the last wave holds one window)
     [(20, 20, 5_001), (12, 13, 3_007), (19, 20, 2_203), (15, 16, 4_111), (25, 8, 2_600)],
