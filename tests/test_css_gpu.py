@@ -290,3 +290,24 @@ def test_fp32_prefilter_changes_no_p(asize, bsize, treshold, runs, nsnp, dup, mo
     assert np.array_equal(s, s2)
     assert (s != 0).sum() > 10
     assert np.array_equal(p, p2), np.flatnonzero(p != p2)[:10]
+
+
+@pytest.mark.parametrize("asize,bsize,nsnp,serial", [(20, 20, 20_000, False), (12, 12, 20_000, False),
+                                                     (40, 40, 6_000, False), (80, 70, 2_000, True)])
+def test_fill_averages_discards(oracle, asize, bsize, nsnp, serial):
+    """Windows whose count matrix is more than half zeros are discarded (fill_averages,
+    css.c:337-366; outputs untouched): a stretch of the chromosome where every individual
+    carries the same genotype has all-zero counts, its edges partly.  The computed-window
+    set and the scores must equal the oracle's in every tier, discarded and computed
+    windows sharing the waves of the 40 tier (one window per half wave)."""
+    from gdscan import css
+    av, bv, ap, bp, regend = _synth(30 + asize, nsnp, asize, bsize)
+    av, bv = av.copy(), bv.copy()
+    lo, hi = regend // 3, regend // 2
+    av[(ap >= lo) & (ap < hi)] = 3.0
+    bv[(bp >= lo) & (bp < hi)] = 3.0
+    s, p = css.scan(av, bv, ap, bp, regend, runs=0, serial=serial)
+    s_ref, p_ref = oracle_css_scan(oracle, av, bv, ap, bp, regend, runs=0, serial=serial)
+    _cmp_scores(s, s_ref)
+    w0, w1 = lo // 500, (hi - 2500) // 500
+    assert np.all(s[w0 + 1:w1] == 0) and (s != 0).sum() > 0  # the uniform stretch is discarded
