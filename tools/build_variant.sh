@@ -1,9 +1,9 @@
 #!/bin/bash
-# Build an A/B variant of libgdscan.so: csrc/gd_css_kernels.hip (or $SRC) recompiled with
+# Build an A/B variant of libgdscan.so: csrc/gd_css_t80.hip (or $SRC) recompiled with
 # extra flags, linked with the other objects of the regular build.
 # usage: tools/build_variant.sh NAME "-DGD_CSS_PROFILE ..."   -> varlib/NAME/libgdscan.so (git-ignored; delete after the A/B session: it travels with every gpurun call)
 set -e
-NAME=$1; FLAGS=$2; SRC=${SRC:-gd_css_kernels}
+NAME=$1; FLAGS=$2; SRC=${SRC:-gd_css_t80}
 P=$(cd "$(dirname "$0")/.." && pwd)/fast-parallel-tools-for-genome-wide-analysis-of-genomic-divergence_amd
 OUT=$(cd "$(dirname "$0")/.." && pwd)/varlib/$NAME
 mkdir -p "$OUT"
