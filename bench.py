@@ -51,7 +51,6 @@ sys.path.insert(0, str(PKG))
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, HBM3E spec
 FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 vector spec
-MFMA_I8_PEAK_TOPS = 5000.0  # MI355X_MICROARCH.md: I8 MFMA at 2x the BF16 rate (~2.5 PF dense)
 # The one VALU ceiling every figure here uses: one wave64 instruction per SIMD per 2 cycles at the
 # 2.4 GHz peak clock, 1024 SIMDs -- the rate of the fastest instruction class (the 2-cycle ops of
 # tools/ubench_valu.hip: v_lshrrev_b32, v_add_f32, v_max_u16 ... 880-994 G/s at the held ~2.1 GHz).
@@ -531,7 +530,9 @@ def dist_build(shape_key, m, kernel_ms, windows):
     (compare_all, css.c:277-327) over the time the bit planes (k_css_pack) plus the
     popcount distance build take -- the build's share of the MDS kernel from the
     committed GD_CSS_PROFILE phase profile, k_css_pack's share of the stage from the
-    kernel trace -- against the MFMA int8 dense peak it would have used."""
+    kernel trace.  The build runs on the VALU (64-bit AND + popcount over the bit planes,
+    64 SNP products per instruction), not on the matrix cores, so no MFMA peak is quoted
+    for it: the figure is its share of the window time and its integer-op rate."""
     if not CSS_PHASE_FILE.exists():
         return None
     doc = json.loads(CSS_PHASE_FILE.read_text()).get(shape_key)
@@ -540,8 +541,9 @@ def dist_build(shape_key, m, kernel_ms, windows):
     share = doc["pack_share"] + (1.0 - doc["pack_share"]) * doc["d_share"]
     ms = kernel_ms * share
     ops = 4.0 * m * m * doc["npos_mean"]
-    return {"ops_per_window": ops, "share_of_window_time": share, "ms": ms,
-            "tops": ops * windows / (ms * 1e-3) / 1e12 if ms > 0 else None, "mfma_int8_peak_tops": MFMA_I8_PEAK_TOPS,
+    return {"unit": "VALU popcount (bit-plane AND + popcount, no MFMA)", "int_ops_per_window": ops,
+            "share_of_window_time": share, "ms": ms,
+            "int_tops_valu": ops * windows / (ms * 1e-3) / 1e12 if ms > 0 else None,
             "pack_share": doc["pack_share"], "d_share_of_mds": doc["d_share"]}
 
 

@@ -157,6 +157,7 @@ struct gd_ctx {
   unsigned *h_flags_dev = nullptr; /* one device word (packer status) */
   char *h_pack = nullptr;          /* pinned: host-packed tracks of the reference-signature calls */
   size_t h_pack_cap = 0;
+  bool pack_inflight = false; /* copies out of h_pack may still run (a call returned mid-upload) */
 };
 
 static int ctx_init(gd_ctx *c, int device) {
@@ -646,10 +647,9 @@ static int fet_scan_locked(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, cons
     HIP_TRY(hipStreamSynchronize(s));
   }
   float ms;
-  /* stage times (HIP events from the scan's first kernel): MEM = the prologue (scheduled
-   * scan: setup, per-SNP pass; grouped: every group's bounds / per-SNP passes), WINDOW = the
-   * end of the last fast window kernel (scheduled: incl. the bounds workers), GENERAL = the
-   * literal path after it, TOTAL */
+  /* stage times (HIP events from the scan's first kernel): MEM = the prologue (setup and
+   * every group's bounds / per-SNP passes), WINDOW = the end of the last fast window kernel,
+   * GENERAL = the literal path after it, TOTAL */
   if (hipEventElapsedTime(&ms, ctx->ev[0], ctx->ev[1]) == hipSuccess) g_stage_ms[GD_STAGE_MEM] = ms;
   if (hipEventElapsedTime(&ms, ctx->ev[0], ctx->ev[2]) == hipSuccess) g_stage_ms[GD_STAGE_WINDOW] = ms;
   if (hipEventElapsedTime(&ms, ctx->ev[2], ctx->ev[3]) == hipSuccess) g_stage_ms[GD_STAGE_GENERAL] = ms;
@@ -724,6 +724,12 @@ static int host_packed(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, const do
     nw = std::max<int64_t>(nw, h.w_out + std::max(h.regend, 0) / wstep);
   }
   if (nw == 0) return GD_OK;
+  /* an earlier call that returned between its uploads (a failed HIP call) may have left DMA
+   * reading the pinned buffer: drain it before the packer threads overwrite it */
+  if (ctx->pack_inflight) {
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    ctx->pack_inflight = false;
+  }
   /* pinned layout: A codes, B codes, row positions */
   const size_t ba = sizeof(uint64_t) * std::max<int64_t>(wa_tot, 1), bb = sizeof(uint64_t) * std::max<int64_t>(wb_tot, 1);
   const size_t br = sizeof(int32_t) * std::max<int64_t>(rows, 1), need = ba + bb + br + 512;
@@ -750,6 +756,7 @@ static int host_packed(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, const do
   HIP_TRY(hipMemcpyAsync(o1, out1, sizeof(double) * nw, hipMemcpyHostToDevice, s));
   /* chunks of ~8M genotypes: chunk j's codes cross PCIe (DMA from pinned memory) while the
    * host threads pack chunk j + 1 */
+  ctx->pack_inflight = true;
   for (int c = 0; c < nchrom; ++c) {
     const gd_chrom &h = chroms[c];
     const gd_pchrom &q = pc[c];
@@ -765,6 +772,7 @@ static int host_packed(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, const do
         g_err = saved;
         g_status = saved_st;
         HIP_TRY(hipStreamSynchronize(s)); /* the chunks already on their way read the pinned buffer */
+        ctx->pack_inflight = false;
         return GD_HOST_NOPACK;
       }
       HIP_TRY(hipMemcpyAsync(ca + q.a_word + r0 * wa, hac + q.a_word + r0 * wa, sizeof(uint64_t) * (r1 - r0) * wa,
@@ -777,12 +785,13 @@ static int host_packed(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, const do
   }
   const PackedIn pk{pc.data(), ca, cb, rp};
   if ((st = run(ctx, pk, nchrom, o0, o1, s))) {
-    (void)hipStreamSynchronize(s); /* the pinned buffer may still be read */
+    if (hipStreamSynchronize(s) == hipSuccess) ctx->pack_inflight = false; /* the pinned buffer may still be read */
     return st;
   }
   HIP_TRY(hipMemcpyAsync(out0, o0, sizeof(double) * nw, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipMemcpyAsync(out1, o1, sizeof(double) * nw, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
+  ctx->pack_inflight = false;
   return GD_OK;
 }
 
@@ -1097,7 +1106,7 @@ static int css_scan_locked(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, cons
   const int mp = gd_css_tier(mmax);
   if (mp == 0) return fail(GD_ERR_SIZE, "asize + bsize above the largest supported cohort (GD_CSS_BIG_MAX = 2048)");
   if (mds != 0 && mp > GD_CSS_SMACOF_MAX)
-    return fail(GD_ERR_SIZE, "SMACOF (mds 1 / 2) above the largest supported cohort (GD_CSS_SMACOF_MAX = 1024)");
+    return fail(GD_ERR_SIZE, "SMACOF (mds 1 / 2) above the largest supported cohort (GD_CSS_SMACOF_MAX)");
   /* the general path (m above the register tiers): one matrix slab per workgroup */
   const int64_t slab_doubles = mp > GD_CSS_TIER_MAX ? gd_css_big_grid(pl.wtotal, mp) * gd_css_big_slab_per_wg(mp) : 1;
   if (drosophila)

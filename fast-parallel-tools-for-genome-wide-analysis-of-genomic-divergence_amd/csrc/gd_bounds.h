@@ -1,9 +1,8 @@
 /*
  * gd_bounds.h -- slide_right() (comparative.c:49-71) for every window of one population of
  * one chromosome, one wave-segment at a time.  Shared by the stand-alone pass k_bounds
- * (gd_fet_kernels.hip; CSS scans and the diagnostic FET shapes) and the bounds workers of
- * the scheduled FET window kernel (gd_fet_fast.hip), which run the same segments beside
- * the bootstrap.
+ * (gd_fet_kernels.hip), which every FET and CSS scan runs once per chromosome group before
+ * its window kernels.
  *
  * lo = first idx with pos >= start, hi = first idx with pos > start + wsize (inclusive
  * end).  Element i owns the windows whose start lies in (pos[i-1], pos[i]] (lo) and whose
@@ -63,34 +62,22 @@ struct gd_bounds_job {
     return gd_fdiv_fast(a, wstep, inv);
   }
 
-  /* COH: the window kernel's bounds workers, whose ranges other workgroups read while the
-   * kernel runs -- stores at device scope (written through the XCD's L2, which is not
-   * coherent with the other XCDs' within a kernel) */
-  template <bool COH>
-  __device__ __forceinline__ static void put(int32_t *p, int32_t v) {
-    if constexpr (COH)
-      __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    else
-      *p = v;
-  }
-
   /* element i (a boundary: i == 0, i == len or pos[i] != pos[i-1]) with p = pos[i] (i < len)
    * and pp = pos[i-1] (i > 0) */
-  template <bool COH>
   __device__ __forceinline__ void own(int64_t i, int64_t p, int64_t pp) const {
     const bool first = (i == 0), last = (i == len);
     int64_t f = first ? 0 : fl(pp) + 1;
     int64_t l = last ? wend - 1 : fl(p);
     if (f < 0) f = 0;
     if (l > wend - 1) l = wend - 1;
-    for (int64_t w = f; w <= l; ++w) put<COH>(lo + w, (int32_t)i);
+    for (int64_t w = f; w <= l; ++w) lo[w] = (int32_t)i;
     if (pop == 0) {
       /* -floor((wsize - x) / wstep) = ceil((x - wsize) / wstep) = floor((x - wsize + wstep - 1) / wstep) */
       f = first ? 0 : fl(pp - wsize + wstep - 1);
       l = last ? wend - 1 : fl(p - wsize + wstep - 1) - 1;
       if (f < 0) f = 0;
       if (l > wend - 1) l = wend - 1;
-      for (int64_t w = f; w <= l; ++w) put<COH>(hi + w, (int32_t)i);
+      for (int64_t w = f; w <= l; ++w) hi[w] = (int32_t)i;
     }
   }
 
@@ -113,7 +100,7 @@ struct gd_bounds_job {
     for (int k = 0; k < CH; ++k) v[k] = *reinterpret_cast<const int4 *>(pos + seg + 256 * k + 4 * lane);
     before = seg > 0 ? pos[seg - 1] : 0; /* element 0 has no predecessor (process: v[0].x) */
   }
-  template <int CH, bool COH>
+  template <int CH>
   __device__ __forceinline__ bool process(int64_t seg, const int4 (&v)[CH], int32_t before, int32_t *sg) const {
     static_assert(CH >= 1 && 4 * CH <= 32, "the boundary mask holds 4 CH bits in a uint32_t");
     const int lane = threadIdx.x & 63;
@@ -145,7 +132,7 @@ struct gd_bounds_job {
         const int b = __builtin_ctz(bits);
         bits &= bits - 1;
         const int r = 256 * (b >> 2) + 4 * lane + (b & 3);
-        own<COH>(seg + r, sg[r], r > 0 ? sg[r - 1] : before);
+        own(seg + r, sg[r], r > 0 ? sg[r - 1] : before);
       }
       __builtin_amdgcn_wave_barrier(); /* the slice is rewritten by the next segment */
     } else {
@@ -153,12 +140,12 @@ struct gd_bounds_job {
         const int b = __builtin_ctz(bits);
         bits &= bits - 1;
         const int64_t i = seg + 256 * (b >> 2) + 4 * lane + (b & 3);
-        own<COH>(i, pos[i], i > 0 ? pos[i - 1] : 0);
+        own(i, pos[i], i > 0 ? pos[i - 1] : 0);
       }
     }
     return dec;
   }
-  template <int CH, bool COH>
+  template <int CH>
   __device__ __forceinline__ bool partial(int64_t seg) const {
     constexpr int SEG = 256 * CH;
     const int lane = threadIdx.x & 63;
@@ -170,19 +157,19 @@ struct gd_bounds_job {
         const int32_t v = (i < len) ? pos[i] : 0;
         const bool bnd = (i == 0) || (i == len) || (v != prev);
         if (i > 0 && i < len) unsorted |= (v < prev);
-        if (bnd) own<COH>(i, v, prev);
+        if (bnd) own(i, v, prev);
         prev = v;
       }
     }
     return unsorted;
   }
-  template <int CH, bool COH = false>
+  template <int CH>
   __device__ __forceinline__ bool segment(int64_t seg, int32_t *sg) const {
-    if (!full<CH>(seg)) return partial<CH, COH>(seg);
+    if (!full<CH>(seg)) return partial<CH>(seg);
     int4 v[CH];
     int32_t before;
     load<CH>(seg, v, before);
-    return process<CH, COH>(seg, v, before, sg);
+    return process<CH>(seg, v, before, sg);
   }
 };
 

@@ -550,61 +550,142 @@ __device__ __forceinline__ void invit_solve(int m, int e, double (*s_lu)[3][MP],
   }
 }
 
+/* two all-reduces over each 32-lane half at once (every lane of a half ends with the same bits) */
+template <class Op>
+__device__ __forceinline__ void half_reduce2(double &a, double &b) {
+  a = Op::op(a, dpp64<0xB1, 0xF>(a, 0.0)); /* quad_perm [1,0,3,2] */
+  b = Op::op(b, dpp64<0xB1, 0xF>(b, 0.0));
+  a = Op::op(a, dpp64<0x4E, 0xF>(a, 0.0)); /* quad_perm [2,3,0,1] */
+  b = Op::op(b, dpp64<0x4E, 0xF>(b, 0.0));
+  a = Op::op(a, dpp64<0x141, 0xF>(a, 0.0)); /* row_half_mirror: quad 0 <-> quad 1 of each 8 */
+  b = Op::op(b, dpp64<0x141, 0xF>(b, 0.0));
+  a = Op::op(a, dpp64<0x140, 0xF>(a, 0.0)); /* row_mirror: the two 8-lane groups of a row */
+  b = Op::op(b, dpp64<0x140, 0xF>(b, 0.0));
+  /* rows 0 + 1 and 2 + 3: both operands of the swap are the row sums, so lane i of row 0
+   * and lane i of row 1 add the same two values in the same order */
+  const uint64_t ua = __builtin_bit_cast(uint64_t, a), ub = __builtin_bit_cast(uint64_t, b);
+  const auto al = __builtin_amdgcn_permlane16_swap((uint32_t)ua, (uint32_t)ua, false, false);
+  const auto ah = __builtin_amdgcn_permlane16_swap((uint32_t)(ua >> 32), (uint32_t)(ua >> 32), false, false);
+  const auto bl = __builtin_amdgcn_permlane16_swap((uint32_t)ub, (uint32_t)ub, false, false);
+  const auto bh = __builtin_amdgcn_permlane16_swap((uint32_t)(ub >> 32), (uint32_t)(ub >> 32), false, false);
+  a = Op::op(__builtin_bit_cast(double, ((uint64_t)ah[0] << 32) | al[0]),
+             __builtin_bit_cast(double, ((uint64_t)ah[1] << 32) | al[1]));
+  b = Op::op(__builtin_bit_cast(double, ((uint64_t)bh[0] << 32) | bl[0]),
+             __builtin_bit_cast(double, ((uint64_t)bh[1] << 32) | bl[1]));
+}
+__device__ __forceinline__ void half_sum2(double &a, double &b) { half_reduce2<OpSum>(a, b); }
+
 /* Eigenvectors of T for the shifts sig0 / sig1 (the two bisection results) by twisted
  * factorisations T - sig I = N_r Delta_r N_r^T (Parlett & Dhillon's solution of
- * Wilkinson's problem), for one wave whose rows are k = lane, lane + 64, ...:
- *   - forward pivots D+_k = p_k / p_{k-1} from the leading minors' recurrence
- *     p_k = (d_k - sig) p_{k-1} - e_{k-1}^2 p_{k-2} (rescaled every 4 steps) and backward
- *     pivots D-_k from the trailing minors: four serial chains (eigenvector x direction)
- *     on lanes 0..3 whose only dependent operation is the FMA; the division that forms
- *     the pivot is off the chain;
- *   - gamma_k = D+_k + D-_k - (d_k - sig) on every row in parallel, r = argmin |gamma_k|;
- *   - z_r = 1, z_k = prod (-e_j / D+_j) above r and prod (-e_{j-1} / D-_j) below it: the
- *     multipliers on every row in parallel, the products as two more chains of multiplies;
+ * Wilkinson's problem), W windows per wave (1, or 2 on the halves), rows k = lane, lane + 64/W:
+ *   - the leading minors p+_k = (d_k - sig) p+_{k-1} - e_{k-1}^2 p+_{k-2} and the trailing
+ *     minors p-_k: four serial chains per window (eigenvector x direction) on lanes 0..3
+ *     of the window whose only dependent operation is the FMA (rescaled by a power of two
+ *     every 4 steps); each step stores its minor, and the pivots D_k = p_k / p_{k-1} are
+ *     formed later on every row in parallel (twist_prev: the rescale exponent is a function
+ *     of the two stored minors before it, so it is recomputed, not stored);
+ *   - gamma_k = D+_k + D-_k - (d_k - sig) on every row, r = argmin |gamma_k|;
+ *   - z_r = 1, z_k = prod_{j=k}^{r-1} (-e_j / D+_j) above r and prod_{j=r+1}^{k} (-e_{j-1} / D-_j)
+ *     below it: the multipliers on every row, the products as four segmented scans per
+ *     window (16 / W lanes each: NB walking steps per lane, a DPP row_shr scan of the block
+ *     products, the block applied);
  *   - sig += gamma_r / |z|^2, the Rayleigh quotient of z ((T - sig I) z = gamma_r e_r).
  * Two rounds.  From the bisection shift (within CSS_BISECT_TOL ||T||) the first gives
  * |z - q| ~ shift error / gap and a Rayleigh shift accurate to its square; the second
  * converges to rounding (worst 4e-13 against LAPACK on 6,000 synthetic 40+40 / 20+20
- * windows, where two pivoted-LU inverse-iteration solves reach 3e-12).  The four chains
- * replace invit_factor's 80-step pivoted elimination (compare, select, reciprocal and
- * FMA on the chain) and invit_solve's 2 x 160 steps.
- * On return s_z[e] holds z (z_r = 1) and nz_e = |z|^2.  False (wave-uniform) when any
- * pivot, multiplier or norm is not finite -- an exactly singular leading or trailing
- * minor -- and the caller falls back to pivoted-LU inverse iteration.  s_e2 carries
- * e_{k-1}^2 floored at CSS_E2_FLOOR at k = 1 .. m - 1 and 0 at k = m. */
-template <int MP>
-__device__ __forceinline__ bool twisted_top2(int m, int lane, const double *s_d, const double *s_e, const double *s_e2,
-                                             double sig0, double sig1, double (*s_D)[2][MP], double (*s_z)[MP],
-                                             double &nz0, double &nz1) {
+ * windows, where two pivoted-LU inverse-iteration solves reach 3e-12).  This replaces
+ * invit_factor's pivoted elimination (compare, select, reciprocal and FMA on the chain)
+ * and invit_solve's 2 x 2m steps.
+ * Per window x: s_d + x sdS, s_e + x seS, s_e2 + x se2S (e_{k-1}^2 floored at CSS_E2_FLOOR
+ * at k = 1 .. m - 1, 0 at k = 0 and k = m), s_lam[2x + e] the shifts; s_rev + x srS (2 MP
+ * doubles of free scratch) takes d and e^2 in backward order so both chain directions walk
+ * upward.  s_Q[x][e][0][k] = p+_k, s_Q[x][e][1][t] = p-_k at t = m - 1 - k; on return
+ * s_Q[x][e][1][k] holds z (z_r = 1) and nz_e = |z|^2 of the lane's window.  False
+ * (wave-uniform) when a pivot, multiplier or norm is not finite -- an exactly singular
+ * leading or trailing minor, or a product out of range: the caller falls back to
+ * pivoted-LU inverse iteration. */
+__device__ __forceinline__ double dpp_shr_f64(double v, int n) { /* n = 1, 2, 4, 8 */
+  const uint64_t u = __builtin_bit_cast(uint64_t, v);
+  uint32_t lo, hi;
+  /* lanes whose source lies before their 16-lane row keep 1.0 (the product identity) */
+  switch (n) {
+    case 1:
+      lo = __builtin_amdgcn_update_dpp(0u, (uint32_t)u, 0x111, 0xF, 0xF, false);
+      hi = __builtin_amdgcn_update_dpp(0x3ff00000u, (uint32_t)(u >> 32), 0x111, 0xF, 0xF, false);
+      break;
+    case 2:
+      lo = __builtin_amdgcn_update_dpp(0u, (uint32_t)u, 0x112, 0xF, 0xF, false);
+      hi = __builtin_amdgcn_update_dpp(0x3ff00000u, (uint32_t)(u >> 32), 0x112, 0xF, 0xF, false);
+      break;
+    case 4:
+      lo = __builtin_amdgcn_update_dpp(0u, (uint32_t)u, 0x114, 0xF, 0xF, false);
+      hi = __builtin_amdgcn_update_dpp(0x3ff00000u, (uint32_t)(u >> 32), 0x114, 0xF, 0xF, false);
+      break;
+    default:
+      lo = __builtin_amdgcn_update_dpp(0u, (uint32_t)u, 0x118, 0xF, 0xF, false);
+      hi = __builtin_amdgcn_update_dpp(0x3ff00000u, (uint32_t)(u >> 32), 0x118, 0xF, 0xF, false);
+  }
+  return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+
+/* the pivot p_t / p_{t-1} of a chain's step t, p_{t-1} brought to step t's scale (the chains
+ * rescale after steps 3, 7, 11, ... by the exponent of max(|p_{t-2}|, |p_{t-1}|)) */
+__device__ __forceinline__ double twist_pivot(const double *Q, int t) {
+  const double p = Q[t];
+  if (t == 0) return p;
+  double q = Q[t - 1];
+  if ((t & 3) == 0) q = __builtin_amdgcn_ldexp(q, -__builtin_amdgcn_frexp_exp(fmax(fabs(Q[t - 2]), fabs(q))));
+  return p * fast_rcp(q);
+}
+
+template <int MP, int W>
+__device__ __forceinline__ bool twisted_top2(const int *M, int lane, const double *s_d, int sdS, const double *s_e,
+                                             int seS, const double *s_e2, int se2S, const double *s_lam,
+                                             double (*s_Q)[2][2][MP], double *s_rev, int srS, double &nz0,
+                                             double &nz1) {
+  static_assert(W == 1 || W == 2, "one window per wave or per half wave");
+  constexpr int G = 64 / W;               /* lanes per window */
+  constexpr int NR = (MP + G - 1) / G;    /* rows per lane */
+  constexpr int LS = 16 / W;              /* lanes per scan segment (4 segments per window) */
+  constexpr int NB = (MP + LS - 1) / LS;  /* walking steps per scan lane */
+  const int x = W == 1 ? 0 : lane / G, ll = lane % G;
+  const int m = W == 1 ? M[0] : (x ? M[1] : M[0]);
+  const double *dX = s_d + x * sdS, *eX = s_e + x * seS, *e2X = s_e2 + x * se2S;
+  double *revX = s_rev + x * srS;
+  double(*Q)[2][MP] = s_Q[x];
+  double sig0 = s_lam[2 * x], sig1 = s_lam[2 * x + 1];
+  for (int k = ll; k < m; k += G) {
+    revX[k] = dX[m - 1 - k];
+    revX[MP + k] = e2X[m - k];
+  }
+  __syncthreads();
   for (int rd = 0; rd < 2; ++rd) {
-    /* pivots: lane 2e + dir, dir 0 forward (k = t), dir 1 backward (k = m - 1 - t; its
-     * e^2 is e_k^2 = s_e2[k + 1], 0 at the first step) */
-    if (lane < 4) {
-      const int e = lane >> 1, dir = lane & 1;
+    /* chains: lane 2e + dir of the window, step t = row t (dir 0) or row m - 1 - t (dir 1) */
+    if (ll < 4) {
+      const int e = ll >> 1, dir = ll & 1;
       const double sig = e ? sig1 : sig0;
-      double *Dk = s_D[e][dir];
-      const int k0 = dir ? m - 1 : 0, ks = dir ? -1 : 1;
+      const double *dd = dir ? revX : dX, *ee = dir ? revX + MP : e2X;
+      double *out = Q[e][dir];
+      const int mc = max(m, 1);
       double pm = 1.0, pc = 1.0;
       double dv[4], ev[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        const int k = k0 + ks * min(u, m - 1);
-        dv[u] = s_d[k];
-        ev[u] = s_e2[k + dir];
+        dv[u] = dd[min(u, mc - 1)];
+        ev[u] = ee[min(u, mc - 1)];
       }
       for (int t0 = 0; t0 < m; t0 += 4) {
         double nd[4], ne[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-          const int k = k0 + ks * min(t0 + 4 + u, m - 1);
-          nd[u] = s_d[k];
-          ne[u] = s_e2[k + dir];
+          nd[u] = dd[min(t0 + 4 + u, mc - 1)];
+          ne[u] = ee[min(t0 + 4 + u, mc - 1)];
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           if (t0 + u < m) {
             const double pn = fma(dv[u] - sig, pc, -(ev[u] * pm));
-            Dk[k0 + ks * (t0 + u)] = pn * fast_rcp(pc); /* pc = 0: not finite, caught below */
+            out[t0 + u] = pn;
             pm = pc;
             pc = pn;
           }
@@ -620,79 +701,121 @@ __device__ __forceinline__ bool twisted_top2(int m, int lane, const double *s_d,
       }
     }
     __syncthreads();
-    /* twist indices: the smallest |gamma_k| (a NaN never compares smaller) */
+    /* pivots of the lane's rows (registers), twist indices: the smallest |gamma_k| (a NaN
+     * never compares smaller) */
+    double Dp0[NR], Dm0[NR], Dp1[NR], Dm1[NR];
     double g0 = __builtin_huge_val(), g1 = __builtin_huge_val();
     int i0 = 0, i1 = 0;
-    for (int k = lane; k < m; k += 64) {
-      const double dk = s_d[k];
-      const double a0 = fabs(s_D[0][0][k] + s_D[0][1][k] - (dk - sig0));
-      const double a1 = fabs(s_D[1][0][k] + s_D[1][1][k] - (dk - sig1));
-      if (a0 < g0) {
-        g0 = a0;
-        i0 = k;
-      }
-      if (a1 < g1) {
-        g1 = a1;
-        i1 = k;
-      }
-    }
-    const double mn0 = wave_reduce<OpMin>(g0), mn1 = wave_reduce<OpMin>(g1);
-    if (!(mn0 < __builtin_huge_val() && mn1 < __builtin_huge_val())) return false;
-    const int r0 = __builtin_amdgcn_readlane(i0, __builtin_ctzll(__ballot(g0 == mn0)));
-    const int r1 = __builtin_amdgcn_readlane(i1, __builtin_ctzll(__ballot(g1 == mn1)));
-    const double gr0 = s_D[0][0][r0] + s_D[0][1][r0] - (s_d[r0] - sig0);
-    const double gr1 = s_D[1][0][r1] + s_D[1][1][r1] - (s_d[r1] - sig1);
-    __syncthreads();
-    /* multipliers in place: -e_k / D+_k above the twist, -e_{k-1} / D-_k below it */
-    for (int k = lane; k < m; k += 64) {
-      if (k < r0) s_D[0][0][k] = -s_e[k] * fast_rcp(s_D[0][0][k]);
-      if (k > r0) s_D[0][1][k] = -s_e[k - 1] * fast_rcp(s_D[0][1][k]);
-      if (k < r1) s_D[1][0][k] = -s_e[k] * fast_rcp(s_D[1][0][k]);
-      if (k > r1) s_D[1][1][k] = -s_e[k - 1] * fast_rcp(s_D[1][1][k]);
-    }
-    __syncthreads();
-    /* z: lane 2e + dir walks away from r_e (dir 0 up to row 0, dir 1 down to row m - 1) */
-    {
-      const int nmax = max(max(r0, m - 1 - r0), max(r1, m - 1 - r1));
-      if (lane < 4) {
-        const int e = lane >> 1, dir = lane & 1;
-        const int r = e ? r1 : r0, cnt = dir ? m - 1 - r : r, ks = dir ? 1 : -1;
-        const double *G = s_D[e][dir];
-        double *zz = s_z[e];
-        if (dir == 0) zz[r] = 1.0;
-        double z = 1.0;
-        double gv[4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) gv[u] = G[min(max(r + ks * (u + 1), 0), m - 1)];
-        for (int t0 = 0; t0 < nmax; t0 += 4) {
-          double ng[4];
-#pragma unroll
-          for (int u = 0; u < 4; ++u) ng[u] = G[min(max(r + ks * (t0 + 5 + u), 0), m - 1)];
-#pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            if (t0 + u < cnt) {
-              z *= gv[u];
-              zz[r + ks * (t0 + u + 1)] = z;
-            }
-          }
-#pragma unroll
-          for (int u = 0; u < 4; ++u) gv[u] = ng[u];
+    for (int q = 0; q < NR; ++q) {
+      const int k = ll + G * q;
+      Dp0[q] = Dm0[q] = Dp1[q] = Dm1[q] = 1.0;
+      if (k < m) {
+        Dp0[q] = twist_pivot(Q[0][0], k);
+        Dm0[q] = twist_pivot(Q[0][1], m - 1 - k);
+        Dp1[q] = twist_pivot(Q[1][0], k);
+        Dm1[q] = twist_pivot(Q[1][1], m - 1 - k);
+        const double dk = dX[k];
+        const double a0 = fabs(Dp0[q] + Dm0[q] - (dk - sig0)), a1 = fabs(Dp1[q] + Dm1[q] - (dk - sig1));
+        if (a0 < g0) {
+          g0 = a0;
+          i0 = k;
+        }
+        if (a1 < g1) {
+          g1 = a1;
+          i1 = k;
         }
       }
     }
+    double mn0 = g0, mn1 = g1;
+    if constexpr (W == 1) {
+      mn0 = wave_reduce<OpMin>(g0);
+      mn1 = wave_reduce<OpMin>(g1);
+    } else {
+      half_reduce2<OpMin>(mn0, mn1);
+    }
+    if (__any(m > 0 && !(mn0 < __builtin_huge_val() && mn1 < __builtin_huge_val()))) return false;
+    const uint64_t bl0 = __ballot(g0 == mn0), bl1 = __ballot(g1 == mn1);
+    int r0, r1;
+    if constexpr (W == 1) {
+      r0 = __builtin_amdgcn_readlane(i0, __builtin_ctzll(bl0));
+      r1 = __builtin_amdgcn_readlane(i1, __builtin_ctzll(bl1));
+    } else {
+      /* each half's first lane holding its minimum (a half with m = 0 has every bit set:
+       * inf == inf) */
+      const int a0 = __builtin_amdgcn_readlane(i0, __builtin_ctzll(bl0 | (1ull << 31)));
+      const int c0 = __builtin_amdgcn_readlane(i0, 32 + __builtin_ctzll((bl0 >> 32) | (1ull << 31)));
+      const int a1 = __builtin_amdgcn_readlane(i1, __builtin_ctzll(bl1 | (1ull << 31)));
+      const int c1 = __builtin_amdgcn_readlane(i1, 32 + __builtin_ctzll((bl1 >> 32) | (1ull << 31)));
+      r0 = x ? c0 : a0;
+      r1 = x ? c1 : a1;
+    }
+    double gr0 = 0.0, gr1 = 0.0;
+    if (m > 0) {
+      gr0 = twist_pivot(Q[0][0], r0) + twist_pivot(Q[0][1], m - 1 - r0) - (dX[r0] - sig0);
+      gr1 = twist_pivot(Q[1][0], r1) + twist_pivot(Q[1][1], m - 1 - r1) - (dX[r1] - sig1);
+    }
+    /* multipliers into Q[e][0][k] (every minor was read above): -e_k / D+_k above the twist,
+     * -e_{k-1} / D-_k below it */
+#pragma unroll
+    for (int q = 0; q < NR; ++q) {
+      const int k = ll + G * q;
+      if (k < m) {
+        const double ek = k + 1 < m ? eX[k] : 0.0, ekm = k > 0 ? eX[k - 1] : 0.0;
+        Q[0][0][k] = k < r0 ? -ek * fast_rcp(Dp0[q]) : -ekm * fast_rcp(Dm0[q]);
+        Q[1][0][k] = k < r1 ? -ek * fast_rcp(Dp1[q]) : -ekm * fast_rcp(Dm1[q]);
+      }
+    }
+    __syncthreads();
+    /* z into Q[e][1][k] by segmented scans: segment (e, dir) of the window (LS lanes) walks
+     * away from r_e, NB steps per lane */
+    {
+      const int seg = (ll / LS) & 3, e = seg >> 1, dir = seg & 1, ls = ll % LS;
+      const int r = e ? r1 : r0, cnt = m > 0 ? (dir ? m - 1 - r : r) : 0, ks = dir ? 1 : -1;
+      const double *Gm = Q[e][0];
+      double *Z = Q[e][1];
+      double c[NB];
+      double run = 1.0;
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        const int t = NB * ls + j;
+        const double g = t < cnt ? Gm[r + ks * (t + 1)] : 1.0;
+        run *= g;
+        c[j] = run;
+      }
+      double v = run;
+#pragma unroll
+      for (int sh = 1; sh < LS; sh <<= 1) {
+        const double o = dpp_shr_f64(v, sh);
+        v *= (LS == 16 || ls >= sh) ? o : 1.0;
+      }
+      double ex = dpp_shr_f64(v, 1); /* the product of the segment's lower lanes' blocks */
+      if (LS != 16 && ls == 0) ex = 1.0;
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        const int t = NB * ls + j;
+        if (t < cnt) Z[r + ks * (t + 1)] = ex * c[j];
+      }
+      if (m > 0 && dir == 0 && ls == 0) Z[r] = 1.0;
+    }
     __syncthreads();
     double s0 = 0.0, s1 = 0.0;
-    for (int k = lane; k < m; k += 64) {
-      const double z0 = s_z[0][k], z1 = s_z[1][k];
+    for (int k = ll; k < m; k += G) {
+      const double z0 = Q[0][1][k], z1 = Q[1][1][k];
       s0 = fma(z0, z0, s0);
       s1 = fma(z1, z1, s1);
     }
-    wave_sum2(s0, s1);
-    if (!(s0 < __builtin_huge_val() && s1 < __builtin_huge_val())) return false; /* NaN fails too */
+    if constexpr (W == 1)
+      wave_sum2(s0, s1);
+    else
+      half_sum2(s0, s1);
+    if (__any(m > 0 && !(s0 < __builtin_huge_val() && s1 < __builtin_huge_val()))) return false; /* NaN fails too */
     nz0 = s0;
     nz1 = s1;
-    sig0 += gr0 / s0;
-    sig1 += gr1 / s1;
+    if (m > 0) {
+      sig0 += gr0 / s0;
+      sig1 += gr1 / s1;
+    }
   }
   return true;
 }

@@ -196,6 +196,7 @@ struct P40Steps<P40> {
 
 /* 17-section bisection for the two largest eigenvalues of both windows' T, a quarter
  * wave per eigenvalue (bisect_top2 with 16 lanes instead of 32) */
+template <bool ZFIX = true> /* false: FMA-only chain over floored e^2 (bisect_top2) */
 __device__ __forceinline__ void p40_bisect(int mA, int mB, const double *glo, const double *ghi, const double *tol,
                                            const double (*s_d)[P40 + 4], const double (*s_e2)[P40 + 4],
                                            double (*s_lam)[2], int lane) {
@@ -225,7 +226,7 @@ __device__ __forceinline__ void p40_bisect(int mA, int mB, const double *glo, co
 #pragma unroll
       for (int uu = 0; uu < 4; ++uu) {
         double pn = fma(dk[uu] - x, pc, -(ek[uu] * pm));
-        pn = (pn == 0.0) ? -pc * DBL_MIN : pn;
+        if constexpr (ZFIX) pn = (pn == 0.0) ? -pc * DBL_MIN : pn;
         cnt += (int)((__double2hiint(pn) ^ __double2hiint(pc)) < 0);
         pm = pc;
         pc = pn;
@@ -812,30 +813,6 @@ constexpr int H40_MAIN = 32, H40_TS = 10, H40_TSTRIDE = 44; /* rows in VGPRs, ta
 
 /* sums over each 32-lane half, every lane of a half holding the same bits (every stage
  * adds a lane to its mirror image, and IEEE addition commutes) */
-template <class Op>
-__device__ __forceinline__ void half_reduce2(double &a, double &b) {
-  a = Op::op(a, dpp64<0xB1, 0xF>(a, 0.0)); /* quad_perm [1,0,3,2] */
-  b = Op::op(b, dpp64<0xB1, 0xF>(b, 0.0));
-  a = Op::op(a, dpp64<0x4E, 0xF>(a, 0.0)); /* quad_perm [2,3,0,1] */
-  b = Op::op(b, dpp64<0x4E, 0xF>(b, 0.0));
-  a = Op::op(a, dpp64<0x141, 0xF>(a, 0.0)); /* row_half_mirror: quad 0 <-> quad 1 of each 8 */
-  b = Op::op(b, dpp64<0x141, 0xF>(b, 0.0));
-  a = Op::op(a, dpp64<0x140, 0xF>(a, 0.0)); /* row_mirror: the two 8-lane groups of a row */
-  b = Op::op(b, dpp64<0x140, 0xF>(b, 0.0));
-  /* rows 0 + 1 and 2 + 3: both operands of the swap are the row sums, so lane i of row 0
-   * and lane i of row 1 add the same two values in the same order */
-  const uint64_t ua = __builtin_bit_cast(uint64_t, a), ub = __builtin_bit_cast(uint64_t, b);
-  const auto al = __builtin_amdgcn_permlane16_swap((uint32_t)ua, (uint32_t)ua, false, false);
-  const auto ah = __builtin_amdgcn_permlane16_swap((uint32_t)(ua >> 32), (uint32_t)(ua >> 32), false, false);
-  const auto bl = __builtin_amdgcn_permlane16_swap((uint32_t)ub, (uint32_t)ub, false, false);
-  const auto bh = __builtin_amdgcn_permlane16_swap((uint32_t)(ub >> 32), (uint32_t)(ub >> 32), false, false);
-  a = Op::op(__builtin_bit_cast(double, ((uint64_t)ah[0] << 32) | al[0]),
-             __builtin_bit_cast(double, ((uint64_t)ah[1] << 32) | al[1]));
-  b = Op::op(__builtin_bit_cast(double, ((uint64_t)bh[0] << 32) | bl[0]),
-             __builtin_bit_cast(double, ((uint64_t)bh[1] << 32) | bl[1]));
-}
-__device__ __forceinline__ void half_sum2(double &a, double &b) { half_reduce2<OpSum>(a, b); }
-
 /* a half-uniform value of lane L of each half (L wave-uniform) */
 __device__ __forceinline__ double half_lane(double v, int L, bool h) {
   const double v0 = readlane_f64(v, L), v1 = readlane_f64(v, 32 + L);
@@ -1216,6 +1193,10 @@ __global__ void __launch_bounds__(64, CSS_P40_WAVES)
       double y[2][2][MP];
       uint8_t piv[2][2][MP];
     } b;
+    struct {
+      double e2[2][MP + 4]; /* = a.e2: the twisted factorisations read it */
+      double Q[2][2][2][MP];
+    } c;
   } s_u;
   __shared__ __attribute__((aligned(16))) double s_d[2][MP + 4];
   __shared__ double s_e[2][MP], s_tau[2][MP];
@@ -1532,7 +1513,7 @@ __global__ void __launch_bounds__(64, CSS_P40_WAVES)
     }
     for (int k = lane; k < 2 * (MP + 4); k += 64) {
       const int x = k >= MP + 4, kk = x ? k - (MP + 4) : k;
-      s_u.a.e2[x][kk] = (kk >= 1 && kk < M[x]) ? s_e[x][kk - 1] * s_e[x][kk - 1] : 0.0;
+      s_u.a.e2[x][kk] = (kk >= 1 && kk < M[x]) ? fmax(s_e[x][kk - 1] * s_e[x][kk - 1], CSS_E2_FLOOR) : 0.0;
     }
     double nlo = -lo; /* min as a max */
     half_reduce2<OpMax>(nlo, hi_);
@@ -1553,59 +1534,77 @@ __global__ void __launch_bounds__(64, CSS_P40_WAVES)
     }
   }
   __syncthreads();
-  p40_bisect(M[0], M[1], glo, ghi, btol, s_d, s_u.a.e2, s_lam, lane);
+  p40_bisect<!CSS_TWIST>(M[0], M[1], glo, ghi, btol, s_d, s_u.a.e2, s_lam, lane);
   __syncthreads();
 
   CSS_PROF(3);
-  /* ---- eigenvectors of each T: two steps of inverse iteration (lanes 0..3) */
-  if (lane < 4 && M[lane >> 1] > 0) {
-    const int x = lane >> 1, e = lane & 1;
-    invit_factor<MP>(M[x], e, s_d[x], s_e[x], s_lam[x], s_u.b.lu[x], s_x[x], s_u.b.piv[x], s_u.b.y[x]);
-  }
-  __syncthreads();
-#pragma unroll
-  for (int x = 0; x < 2; ++x) {
-    const double tiny = DBL_EPSILON * fmax(fmax(fabs(glo[x]), fabs(ghi[x])), DBL_MIN);
-    for (int k = lane; k < M[x]; k += 64) {
-#pragma unroll
-      for (int e = 0; e < 2; ++e) {
-        const double u0 = s_u.b.lu[x][e][0][k];
-        s_u.b.lu[x][e][0][k] = fast_rcp(u0 == 0.0 ? tiny : u0);
-      }
-    }
-  }
+  /* ---- eigenvectors of each T: twisted factorisations, or two steps of inverse iteration */
   double y1 = 0.0, y2 = 0.0, y1t = 0.0, y2t = 0.0;
-#ifdef GD_CSS_SKIP_INVIT
-  for (int itn = 0; itn < 0; ++itn) {
-#else
-  for (int itn = 0; itn < 2; ++itn) {
-#endif
-    __syncthreads();
-    if (lane < 4 && M[lane >> 1] > 0) {
-      const int x = lane >> 1;
-      invit_solve<MP>(M[x], lane & 1, s_u.b.lu[x], s_x[x], s_u.b.piv[x], s_u.b.y[x]);
+  bool twist_ok = false;
+#if CSS_TWIST
+  {
+    double nz0, nz1;
+    twist_ok = twisted_top2<MP, 2>(M, lane, &s_d[0][0], MP + 4, &s_e[0][0], MP, &s_u.c.e2[0][0], MP + 4, &s_lam[0][0],
+                                   s_u.c.Q, &s_x[0][0], 2 * MP, nz0, nz1);
+    if (twist_ok) {
+      const double r1 = 1.0 / sqrt(nz0), r2 = 1.0 / sqrt(nz1);
+      y1 = rowk ? s_u.c.Q[hi][0][1][r] * r1 : 0.0;
+      y2 = rowk ? s_u.c.Q[hi][1][1][r] * r2 : 0.0;
+      y1t = trowk ? s_u.c.Q[hi][0][1][R] * r1 : 0.0;
+      y2t = trowk ? s_u.c.Q[hi][1][1][R] * r2 : 0.0;
     }
     __syncthreads();
-    y1 = rowk ? s_u.b.y[hi][0][r] : 0.0;
-    y2 = rowk ? s_u.b.y[hi][1][r] : 0.0;
-    y1t = trowk ? s_u.b.y[hi][0][R] : 0.0;
-    y2t = trowk ? s_u.b.y[hi][1][R] : 0.0;
-    double n1 = y1 * y1 + (tq == 0 ? y1t * y1t : 0.0), n2 = y2 * y2 + (tq == 0 ? y2t * y2t : 0.0);
-    half_sum2(n1, n2);
-    const double r1 = 1.0 / sqrt(n1), r2 = 1.0 / sqrt(n2);
-    y1 *= r1;
-    y2 *= r2;
-    y1t *= r1;
-    y2t *= r2;
+  }
+#endif
+  if (!twist_ok) {
+    if (lane < 4 && M[lane >> 1] > 0) {
+      const int x = lane >> 1, e = lane & 1;
+      invit_factor<MP>(M[x], e, s_d[x], s_e[x], s_lam[x], s_u.b.lu[x], s_x[x], s_u.b.piv[x], s_u.b.y[x]);
+    }
     __syncthreads();
-    if (itn == 0) {
-      if (rowk) {
-        s_u.b.y[hi][0][r] = y1;
-        s_u.b.y[hi][1][r] = y2;
+#pragma unroll
+    for (int x = 0; x < 2; ++x) {
+      const double tiny = DBL_EPSILON * fmax(fmax(fabs(glo[x]), fabs(ghi[x])), DBL_MIN);
+      for (int k = lane; k < M[x]; k += 64) {
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const double u0 = s_u.b.lu[x][e][0][k];
+          s_u.b.lu[x][e][0][k] = fast_rcp(u0 == 0.0 ? tiny : u0);
+        }
       }
-      if (tq == 0 && trowk) {
-        s_u.b.y[hi][0][R] = y1t;
-        s_u.b.y[hi][1][R] = y2t;
+    }
+#ifdef GD_CSS_SKIP_INVIT
+    for (int itn = 0; itn < 0; ++itn) {
+#else
+    for (int itn = 0; itn < 2; ++itn) {
+#endif
+      __syncthreads();
+      if (lane < 4 && M[lane >> 1] > 0) {
+        const int x = lane >> 1;
+        invit_solve<MP>(M[x], lane & 1, s_u.b.lu[x], s_x[x], s_u.b.piv[x], s_u.b.y[x]);
+      }
+      __syncthreads();
+      y1 = rowk ? s_u.b.y[hi][0][r] : 0.0;
+      y2 = rowk ? s_u.b.y[hi][1][r] : 0.0;
+      y1t = trowk ? s_u.b.y[hi][0][R] : 0.0;
+      y2t = trowk ? s_u.b.y[hi][1][R] : 0.0;
+      double n1 = y1 * y1 + (tq == 0 ? y1t * y1t : 0.0), n2 = y2 * y2 + (tq == 0 ? y2t * y2t : 0.0);
+      half_sum2(n1, n2);
+      const double r1 = 1.0 / sqrt(n1), r2 = 1.0 / sqrt(n2);
+      y1 *= r1;
+      y2 *= r2;
+      y1t *= r1;
+      y2t *= r2;
+      __syncthreads();
+      if (itn == 0) {
+        if (rowk) {
+          s_u.b.y[hi][0][r] = y1;
+          s_u.b.y[hi][1][r] = y2;
+        }
+        if (tq == 0 && trowk) {
+          s_u.b.y[hi][0][R] = y1t;
+          s_u.b.y[hi][1][R] = y2t;
+        }
       }
     }
   }

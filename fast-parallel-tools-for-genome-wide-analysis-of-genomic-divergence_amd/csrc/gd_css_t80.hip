@@ -293,8 +293,7 @@ __global__ void __launch_bounds__(64, 2)
     } b;
     struct {
       double e2[MP + 4]; /* = a.e2: the twisted factorisations read it */
-      double D[2][2][MP];
-      double z[2][MP];
+      double Q[2][2][MP];
     } c;
   } s_u;
   __shared__ __attribute__((aligned(16))) double s_d[MP + 4];
@@ -590,13 +589,14 @@ __global__ void __launch_bounds__(64, 2)
 #if CSS_TWIST
     {
       double nz0, nz1;
-      twist_ok = twisted_top2<MP>(m, tid, s_d, s_e, s_e2, s_lam[0], s_lam[1], s_u.c.D, s_u.c.z, nz0, nz1);
+      const int M1[1] = {m};
+      twist_ok = twisted_top2<MP, 1>(M1, tid, s_d, 0, s_e, 0, s_e2, 0, s_lam, &s_u.c.Q, s_x, 0, nz0, nz1);
       if (twist_ok) {
         const double r1 = 1.0 / sqrt(nz0), r2 = 1.0 / sqrt(nz1);
-        y1 = row ? s_u.c.z[0][i] * r1 : 0.0;
-        y2 = row ? s_u.c.z[1][i] * r2 : 0.0;
-        y1t = trow ? s_u.c.z[0][R] * r1 : 0.0;
-        y2t = trow ? s_u.c.z[1][R] * r2 : 0.0;
+        y1 = row ? s_u.c.Q[0][1][i] * r1 : 0.0;
+        y2 = row ? s_u.c.Q[1][1][i] * r2 : 0.0;
+        y1t = trow ? s_u.c.Q[0][1][R] * r1 : 0.0;
+        y2t = trow ? s_u.c.Q[1][1][R] * r2 : 0.0;
       }
       __syncthreads();
     }

@@ -86,32 +86,8 @@ __global__ void __launch_bounds__(256) k_bounds(const gd_chrom_dev *ch, const in
   const int64_t wave0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
   bool unsorted = false;
-#ifndef KB_PREFETCH
-#define KB_PREFETCH 0
-#endif
-#if KB_PREFETCH
-  /* the next full segment's loads are issued before this one is walked */
-  int4 v[KB_CH];
-  int32_t before = 0;
-  int64_t seg = wave0 * KB_SEG;
-  bool have = seg <= job.len && job.full<KB_CH>(seg);
-  if (have) job.load<KB_CH>(seg, v, before);
-  for (; seg <= job.len; seg += nwaves * KB_SEG) {
-    const int64_t nx = seg + nwaves * KB_SEG;
-    const bool nhave = nx <= job.len && job.full<KB_CH>(nx);
-    int4 w[KB_CH];
-    int32_t wb = 0;
-    if (nhave) job.load<KB_CH>(nx, w, wb);
-    unsorted |= have ? job.process<KB_CH, false>(seg, v, before, kb_sh[threadIdx.x >> 6]) : job.partial<KB_CH, false>(seg);
-#pragma unroll
-    for (int k = 0; k < KB_CH; ++k) v[k] = w[k];
-    before = wb;
-    have = nhave;
-  }
-#else
   for (int64_t seg = wave0 * KB_SEG; seg <= job.len; seg += nwaves * KB_SEG)
     unsorted |= job.segment<KB_CH>(seg, kb_sh[threadIdx.x >> 6]);
-#endif
   if (unsorted) atomicOr(flags, job.pop ? GD_FLAG_UNSORTED_B : GD_FLAG_UNSORTED_A);
 }
 
@@ -229,7 +205,7 @@ __global__ void k_fet_lut_publish(const gd_chrom_dev *ch, const uint64_t *binom,
   hdr[3] = fet_mode(binom);
 }
 
-/* The prologue of a scheduled FET scan in one launch (gd_api.hip): every chromosome's
+/* The prologue of a grouped FET scan in one launch (gd_api.hip): every chromosome's
  * population sizes (one wave each, as k_popsize), the score table for chromosome 0's sizes
  * when the context does not hold it yet (as k_fet_lut_build; every workgroup derives the
  * sizes itself from the positions, so nothing waits for the size pass), and the header,

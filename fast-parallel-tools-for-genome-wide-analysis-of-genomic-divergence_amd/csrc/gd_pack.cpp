@@ -13,6 +13,7 @@
  * GD_ERR_ARG and keeps the reference layout.
  */
 #include <immintrin.h>
+#include <pthread.h>
 #include <sched.h>
 
 #include <algorithm>
@@ -171,7 +172,12 @@ static int pack_threads() {
 
 /* A persistent pool of host threads for the packer (created on first use, pack_threads()
  * strong with the caller): a job is a number of pieces handed out by a counter; the caller
- * works on pieces too and returns when every piece is done.  One job at a time. */
+ * works on pieces too and returns when every piece is done.  One job at a time, process-wide:
+ * host calls on different contexts or devices from different threads pack one after the
+ * other (their device work still overlaps); the host-path figures in DESIGN.md are single
+ * caller numbers.  A forked child inherits none of the worker threads: the pthread_atfork
+ * child handler leaks their handles (joining threads that do not exist in the child would
+ * hang), re-creates the locks, and the child packs on its calling thread alone. */
 namespace {
 class PackPool {
  public:
@@ -204,7 +210,20 @@ class PackPool {
  private:
   explicit PackPool(int n) {
     for (int t = 1; t < n; ++t) workers_.emplace_back([this] { loop(); });
+    self_ = this;
+    pthread_atfork(nullptr, nullptr, &PackPool::after_fork_child);
   }
+  static void after_fork_child() {
+    PackPool *p = self_;
+    if (!p) return;
+    (void)new std::vector<std::thread>(std::move(p->workers_)); /* never joined or destroyed */
+    p->workers_.clear();
+    new (&p->mu_) std::mutex();
+    new (&p->job_mu_) std::mutex();
+    new (&p->cv_) std::condition_variable();
+    new (&p->cv_done_) std::condition_variable();
+  }
+  static inline PackPool *self_ = nullptr;
   ~PackPool() {
     {
       std::lock_guard<std::mutex> g(mu_);

@@ -1,8 +1,9 @@
 """CPU restatement of the region filters that follow the scans -- TEST INFRASTRUCTURE ONLY.
 
-Only tests/ may import this module (as the checker of gd_fet_region_limit,
-gd_css_fdr_threshold, gd_css_top_limit and gd_merge_regions); the product path never
-calls it.
+Only tests/ and bench.py's CPU-baseline leg (the numpy restatement timed beside the
+device region filters, after the timed steps) may import this module, as the checker
+of gd_fet_region_limit, gd_css_fdr_threshold, gd_css_top_limit and gd_merge_regions;
+the product path never calls it.
 
 Restated from the reference tools (Python 2 + HyperBrowser, not importable here):
   filter_limit      tools/FilterFisherScores.py:83-87

@@ -163,3 +163,56 @@ def test_fet_batch_packed_route():
         assert st == 0, lib.gd_last_error()
         out.append((s, d))
     assert np.array_equal(out[0][0], out[1][0], equal_nan=True) and np.array_equal(out[0][1], out[1][1], equal_nan=True)
+
+
+def _fet_status(av, bv, ap, bp, regend, seed=777, fill=5.0):
+    from gdscan import lib
+    n = regend // 500
+    s, d = np.full(n, fill), np.full(n, fill)
+    st = lib.gd_fet_scan_host(_d(av), _d(bv), _i(ap), _i(bp), regend, 2500, 500, len(av), len(bv), 0.95, seed, 0,
+                              _d(s), _d(d))
+    return st, s, d
+
+
+def _css_status(av, bv, ap, bp, regend, runs=50, seed=777, fill=5.0):
+    from gdscan import lib
+    n = regend // 500
+    s, p = np.full(n, fill), np.full(n, fill)
+    st = lib.gd_css_scan_host_ex(_d(av), _d(bv), _i(ap), _i(bp), regend, 2500, 500, len(av), len(bv), 10, runs, 0, 0,
+                                 seed, 0, _d(s), _d(p))
+    return st, s, p
+
+
+@pytest.mark.parametrize("kind", ["repeat", "decrease"])
+@pytest.mark.parametrize("scan", ["fet", "css"])
+def test_packed_route_row_positions(oracle, kind, scan):
+    """Row positions the packer accepts (A and B rows share them) but slide_right sees as
+    unusual: two consecutive rows at one position (k_bounds_rows' repeated run), and a
+    decreasing position (the packed route's UNSORTED detection, not a fallback).  The packed
+    route must give the reference-layout route's outputs and status."""
+    from gdscan import synth
+    a, b = 12, 9
+    av, bv, ap, bp, regend = synth.chromosome(66, 8000, a, b)
+    ap, bp = ap.copy(), bp.copy()
+    r = 3000
+    if kind == "repeat":
+        ap[a * (r + 1):a * (r + 2)] = ap[a * r]
+        bp[b * (r + 1):b * (r + 2)] = bp[b * r]
+    else:
+        ap[a * (r + 1):a * (r + 2)] = ap[a * r] - 1
+        bp[b * (r + 1):b * (r + 2)] = bp[b * r] - 1
+    run = _fet_status if scan == "fet" else _css_status
+    st1, o1, q1 = run(av, bv, ap, bp, regend)
+    with nopack():
+        st2, o2, q2 = run(av, bv, ap, bp, regend)
+    assert st1 == st2
+    assert np.array_equal(o1, o2, equal_nan=True) and np.array_equal(q1, q2, equal_nan=True)
+    if kind == "repeat":
+        assert st1 == 0 and (o1 != 5.0).sum() > 0
+        if scan == "fet":
+            n = regend // 500
+            s_ref, d_ref = np.full(n, 5.0), np.full(n, 5.0)
+            oracle.orc_fet_scan(av, bv, ap, bp, regend, 2500, 500, len(av), len(bv), 0.95, 777, 0, s_ref, d_ref)
+            assert close(o1, s_ref) and close(q1, d_ref)
+    else:
+        assert st1 != 0  # unsorted positions are reported on both routes

@@ -107,11 +107,15 @@ def test_rccl_device_tensor_gathers_one_rank():
     assert out["css"]["c5"]["resident_input_bytes_per_rank"] == 2 * 60000 * 40 * 24
 
 
-def test_bench_two_ranks_one_gpu():
+def test_bench_two_ranks_one_gpu(tmp_path):
     """bench.py at --gpus 2 as the driver launches it (torch.distributed.run, two ranks),
     both ranks on cuda:0 over gloo: every leg's collectives are entered by every rank in the
     same order (a rank-0-only all-reduce after the other ranks had returned once hung the C5
-    leg), the C5 queue hands every chromosome to exactly one rank, and rank 0 prints the line."""
+    leg), the C5 queue hands every chromosome to exactly one rank, and rank 0 prints the line.
+    Each rank's stdout / stderr go to its own file (torch.distributed.run --log-dir
+    --redirects 3) and a failure reports every rank's stderr tail, so the rank that failed
+    first is named by its own traceback (round 5 lost rank 0's, keeping only the launcher's
+    last 3,000 characters)."""
     import json
     import signal
     import subprocess
@@ -119,20 +123,32 @@ def test_bench_two_ranks_one_gpu():
     from pathlib import Path
     root = Path(__file__).resolve().parent.parent
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    logs = tmp_path / "ranks"
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), str(root / "bench.py"), "--gpus", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "--log-dir", str(logs),
+           "--redirects", "3", str(root / "bench.py"), "--gpus", "2",
            "--steps", "2", "--warmup", "1", "--nchrom", "1", "--nsnp", "60000", "--no-extra", "--css-steps", "1",
            "--c45-chroms", "2", "--c45-steps", "1"]
     p = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env, cwd=root,
                          start_new_session=True)
+
+    def rank_file(rank, name):
+        hits = sorted(logs.glob(f"*/attempt_*/{rank}/{name}"))
+        return hits[-1].read_text(errors="replace") if hits else ""
+
+    def rank_report():
+        return "\n".join(f"--- rank {r} stderr (tail) ---\n{rank_file(r, 'stderr.log')[-4000:]}" for r in (0, 1))
+
     try:
         so, se = p.communicate(timeout=240)
     except subprocess.TimeoutExpired:
         os.killpg(p.pid, signal.SIGKILL)
         p.communicate()
-        raise AssertionError("two-rank bench did not finish in 240 s")
-    assert p.returncode == 0, se[-3000:]
-    out = json.loads(so.strip().splitlines()[-1])
+        raise AssertionError("two-rank bench did not finish in 240 s\n" + rank_report())
+    assert p.returncode == 0, f"launcher: {se[-1500:]}\n{rank_report()}"
+    r0 = rank_file(0, "stdout.log").strip().splitlines()
+    assert r0, "rank 0 wrote no stdout\n" + rank_report()
+    out = json.loads(r0[-1])
     assert out["n_gpus"] == 2 and out["config"]["collective_backend"] == "gloo"
     assert out["config"]["track_gather_ms"] is not None
     assert out["cpu_baseline"]["value"] > 0  # rank 0 times the reference CPU path at N > 1 too
