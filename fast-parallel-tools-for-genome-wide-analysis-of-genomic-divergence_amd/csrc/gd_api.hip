@@ -329,6 +329,7 @@ static int make_plan(const gd_chrom *chroms, int nchrom, int wsize, int wstep, i
   for (int c = 0; c < nchrom; ++c) {
     const gd_chrom &s = chroms[c];
     if (s.alen < 0 || s.blen < 0 || s.a_off < 0 || s.b_off < 0) return fail(GD_ERR_ARG, "negative extent");
+    if (s.w_first < 0 || s.w_count < 0) return fail(GD_ERR_ARG, "negative window range");
     gd_chrom_dev &d = pl->h[c];
     std::memset(&d, 0, sizeof d);
     d.a_off = s.a_off;
@@ -338,7 +339,11 @@ static int make_plan(const gd_chrom *chroms, int nchrom, int wsize, int wstep, i
     d.regend = s.regend;
     d.w_out = s.w_out;
     d.seed = s.seed;
-    d.wend = (s.alen > 0 && s.blen > 0) ? gd_window_count(s.regend, wsize, wstep, window_set) : 0;
+    /* the chromosome's window set [0, n), restricted to [w_first, w_first + w_count) */
+    const int64_t n = (s.alen > 0 && s.blen > 0) ? gd_window_count(s.regend, wsize, wstep, window_set) : 0;
+    const int64_t hi = s.w_count > 0 ? std::min<int64_t>(n, (int64_t)s.w_first + s.w_count) : n;
+    d.w_first = s.w_first;
+    d.wend = (int32_t)std::max<int64_t>(0, hi - s.w_first);
     d.w_base = wb;
     wb += d.wend;
     pl->elems_a = std::max<int64_t>(pl->elems_a, s.a_off + s.alen);
@@ -697,6 +702,7 @@ static int host_packed(gd_ctx *ctx, const gd_chrom *chroms, int nchrom, const do
   int64_t rows = 0, wa_tot = 0, wb_tot = 0, nw = 0;
   for (int c = 0; c < nchrom; ++c) {
     const gd_chrom &h = chroms[c];
+    if (h.w_first != 0 || h.w_count != 0) return GD_HOST_NOPACK; /* window-range shards: reference layout */
     int asz = 0, bsz = 0, nr = 0;
     if (h.alen > 0 && h.blen > 0) {
       const std::string saved = g_err; /* a refusal here is not the call's error */
@@ -881,7 +887,9 @@ static int host_batch(const gd_chrom *chroms, int nchrom, const double *avals, c
       return fail(GD_ERR_ARG, "negative extent");
     na = std::max<int64_t>(na, h.a_off + h.alen);
     nb = std::max<int64_t>(nb, h.b_off + h.blen);
-    nw = std::max<int64_t>(nw, h.w_out + std::max(h.regend, 0) / wstep);
+    /* the caller's output span of this descriptor: its window range (window-range shards) */
+    const int64_t span = std::max<int64_t>(0, std::max(h.regend, 0) / wstep - std::max(h.w_first, 0));
+    nw = std::max<int64_t>(nw, h.w_out + (h.w_count > 0 ? std::min<int64_t>(h.w_count, span) : span));
   }
   if (nchrom == 0 || nw == 0) return GD_OK;
   if (!avals || !bvals || !apos || !bpos || !out0 || !out1) return fail(GD_ERR_ARG, "null buffer");

@@ -24,7 +24,7 @@ __device__ __forceinline__ int64_t gd_fdiv_fast(int64_t a, int32_t b, double inv
 struct gd_bounds_job {
   const int32_t *pos;
   int32_t *lo, *hi; /* hi: A only */
-  int64_t len, wend;
+  int64_t len, wend, wf; /* wf: the chromosome index of local window 0 (window-range shards) */
   int wsize, wstep, pop;
   double inv;
   int kl;
@@ -40,6 +40,7 @@ struct gd_bounds_job {
                                        int wsize_, int wstep_, int32_t *lo_a, int32_t *hi_a, int32_t *lo_b) {
     pop = pop_;
     wend = d.wend;
+    wf = d.w_first;
     len = pop ? d.blen : d.alen;
     pos = pop ? bpos + d.b_off : apos + d.a_off;
     lo = (pop ? lo_b : lo_a) + d.w_base;
@@ -66,15 +67,15 @@ struct gd_bounds_job {
    * and pp = pos[i-1] (i > 0) */
   __device__ __forceinline__ void own(int64_t i, int64_t p, int64_t pp) const {
     const bool first = (i == 0), last = (i == len);
-    int64_t f = first ? 0 : fl(pp) + 1;
-    int64_t l = last ? wend - 1 : fl(p);
+    int64_t f = first ? 0 : fl(pp) + 1 - wf;
+    int64_t l = last ? wend - 1 : fl(p) - wf;
     if (f < 0) f = 0;
     if (l > wend - 1) l = wend - 1;
     for (int64_t w = f; w <= l; ++w) lo[w] = (int32_t)i;
     if (pop == 0) {
       /* -floor((wsize - x) / wstep) = ceil((x - wsize) / wstep) = floor((x - wsize + wstep - 1) / wstep) */
-      f = first ? 0 : fl(pp - wsize + wstep - 1);
-      l = last ? wend - 1 : fl(p - wsize + wstep - 1) - 1;
+      f = first ? 0 : fl(pp - wsize + wstep - 1) - wf;
+      l = last ? wend - 1 : fl(p - wsize + wstep - 1) - 1 - wf;
       if (f < 0) f = 0;
       if (l > wend - 1) l = wend - 1;
       for (int64_t w = f; w <= l; ++w) hi[w] = (int32_t)i;

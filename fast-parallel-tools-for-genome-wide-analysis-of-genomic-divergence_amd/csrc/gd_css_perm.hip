@@ -1077,7 +1077,7 @@ __global__ void __launch_bounds__(PermShape<MP>::NT) PERM_WPE
     }
     PERM_PROF(0);
 
-    uint64_t base = gd_window_state(d.seed, GD_STREAM_CSS, wl);
+    uint64_t base = gd_window_state(d.seed, GD_STREAM_CSS, wl + d.w_first);
     const gd_affine Jq = gd_lcg_jump((uint64_t)tid * (uint64_t)m1), JP = gd_lcg_jump((uint64_t)P * (uint64_t)m1);
     int hits = 0, nsc = 0;
     bool done = !(treshold > 0 && runs > 0);
@@ -1465,7 +1465,7 @@ __global__ void __launch_bounds__(256)
     }
     __syncthreads();
     const double obs = s_obs;
-    uint64_t base = gd_window_state(d.seed, GD_STREAM_CSS, wl);
+    uint64_t base = gd_window_state(d.seed, GD_STREAM_CSS, wl + d.w_first);
     const gd_affine Jq = gd_lcg_jump((uint64_t)lane * (uint64_t)m1), JP = gd_lcg_jump((uint64_t)P * (uint64_t)m1);
     int cur = 0;
     while (!s_ctl[2]) {

@@ -440,7 +440,7 @@ __global__ void __launch_bounds__(sm_nt<MP>())
     Xf = s_z[fin];
   } else {
     /* smacof_runs (css.c:807-835) */
-    const uint64_t x0 = gd_window_state(d.seed, GD_STREAM_SMACOF, wl);
+    const uint64_t x0 = gd_window_state(d.seed, GD_STREAM_SMACOF, wl + d.w_first);
     double best = SM_SIGMA0, fallback = 0.0;
     bool have = false;
     for (int r = 0; r < SM_NINIT; ++r) {

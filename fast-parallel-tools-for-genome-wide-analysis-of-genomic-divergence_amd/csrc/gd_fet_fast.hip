@@ -838,7 +838,7 @@ __global__ void __launch_bounds__(FW_WPB *FW_TPW) FW_WPE
   const int nt = (n > 0 && n <= FW_NFAST) ? n : 1;
   const uint32_t limit = g_ntab_limit[nt];
   uint64_t x0 = 0;
-  if (fast) x0 = gd_window_state(d.seed, GD_STREAM_FET, g - d.w_base);
+  if (fast) x0 = gd_window_state(d.seed, GD_STREAM_FET, g - d.w_base + d.w_first);
   uint16_t *rix = sh_rix[wl] + r0;
 #ifndef GD_FET_NODRAW /* diagnostics: setup cost only */
   if (boot) {

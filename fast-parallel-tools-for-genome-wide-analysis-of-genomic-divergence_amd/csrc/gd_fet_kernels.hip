@@ -455,7 +455,7 @@ __global__ void __launch_bounds__(BLOCK)
 
     /* 3. bootstrap: 100 replicates of n draws from the sorted scores */
     const gd_randint rd = gd_randint_make((uint32_t)n);
-    uint64_t xP = gd_window_state(d.seed, GD_STREAM_FET, w);
+    uint64_t xP = gd_window_state(d.seed, GD_STREAM_FET, w + d.w_first);
     for (int i = tid; i < n; i += BLOCK) hist[i] = 0;
     __syncthreads();
     for (int rep = 0; rep < GD_NREP; ++rep) {

@@ -21,7 +21,7 @@ typedef struct gd_chrom_dev {
   int32_t regend, wend; /* windows [0, wend) are computed */
   int32_t asize, bsize; /* get_population_size(), filled on the device */
   int32_t nrows;        /* min(alen/asize, blen/bsize), filled on the device */
-  int32_t pad_;
+  int32_t w_first;      /* chromosome index of this descriptor's window 0 (window-range shards) */
   uint64_t seed;
 } gd_chrom_dev;
 

@@ -55,16 +55,16 @@ __global__ void __launch_bounds__(256) k_bounds_rows(const gd_chrom_dev *ch, con
     const int64_t p = last ? 0 : pos[r], pp = first ? 0 : pos[r - 1];
     if (!first && !last) unsorted |= p < pp;
     if (!first && !last && p == pp) continue;
-    int64_t f = first ? 0 : pk_fdiv(pp, wstep) + 1;
-    int64_t l = last ? wend - 1 : pk_fdiv(p, wstep);
+    int64_t f = first ? 0 : pk_fdiv(pp, wstep) + 1 - d.w_first;
+    int64_t l = last ? wend - 1 : pk_fdiv(p, wstep) - d.w_first;
     f = f < 0 ? 0 : f;
     l = l > wend - 1 ? wend - 1 : l;
     for (int64_t w = f; w <= l; ++w) {
       lo[w] = (int32_t)(r * d.asize);
       lb[w] = (int32_t)(r * d.bsize);
     }
-    f = first ? 0 : -pk_fdiv(wsize - pp, wstep);
-    l = last ? wend - 1 : -pk_fdiv(wsize - p, wstep) - 1;
+    f = first ? 0 : -pk_fdiv(wsize - pp, wstep) - d.w_first;
+    l = last ? wend - 1 : -pk_fdiv(wsize - p, wstep) - 1 - d.w_first;
     f = f < 0 ? 0 : f;
     l = l > wend - 1 ? wend - 1 : l;
     for (int64_t w = f; w <= l; ++w) hi[w] = (int32_t)(r * d.asize);

@@ -60,8 +60,9 @@ class Chrom(C.Structure):
     _fields_ = [
         ("a_off", C.c_int64), ("b_off", C.c_int64),
         ("alen", C.c_int32), ("blen", C.c_int32),
-        ("regend", C.c_int32), ("pad_", C.c_int32),
+        ("regend", C.c_int32), ("w_first", C.c_int32),
         ("w_out", C.c_int64), ("seed", C.c_uint64),
+        ("w_count", C.c_int32), ("pad_", C.c_int32),
     ]
 
 

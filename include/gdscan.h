@@ -109,10 +109,21 @@ typedef struct gd_chrom {
   int64_t a_off, b_off; /* element offsets of this chromosome in avals/apos and bvals/bpos */
   int32_t alen, blen;   /* element counts */
   int32_t regend;       /* region end (chromosome length); windows are [w*wstep, w*wstep+wsize] */
-  int32_t pad_;
-  int64_t w_out;        /* index in scores/stddev|p of this chromosome's window 0 */
+  int32_t w_first;      /* window-range shard: the first window (chromosome index) this descriptor
+                           computes; 0 = the chromosome's start */
+  int64_t w_out;        /* index in scores/stddev|p of window w_first */
   uint64_t seed;        /* RNG seed of this chromosome's bootstrap / permutations */
+  int32_t w_count;      /* windows computed from w_first on (0 = to the end of the window set) */
+  int32_t pad_;
 } gd_chrom;
+/* A window-range shard (gdscan.shard.plan_window_shards, the reference's 100-window task
+ * with its SNP span, threadfisher.c:106-116, threadcss.c:114-124) is the chromosome's
+ * arrays from the first element at position >= w_first * wstep to the last element a
+ * window of the range reads, with the chromosome's regend and seed: its windows
+ * w_first .. w_first + w_count - 1 of the chromosome's window set are computed, with the
+ * chromosome's per-window seeds, and written at w_out + (w - w_first).  The slice must
+ * start on a whole row (get_population_size reads the first run); outputs equal the
+ * whole-chromosome scan's bit for bit.  Packed batches take w_first = w_count = 0. */
 
 typedef struct gd_ctx gd_ctx;
 gd_ctx *gd_ctx_create(int device); /* NULL on failure */
