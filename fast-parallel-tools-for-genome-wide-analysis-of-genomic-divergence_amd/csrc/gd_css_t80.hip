@@ -427,11 +427,14 @@ __global__ void __launch_bounds__(64, 2)
             }
           }
         }
+        /* rows >= m read stale values: zero them (the popcount path has no bits there) */
+#pragma unroll
+        for (int jj = 0; jj < MP; ++jj) A[jj] = row ? A[jj] : 0.0;
       }
+      /* entries past column m are zero already (no plane bits, or the literal loop's j < m
+       * test), as are main rows >= m: only the tail rows are masked */
       int mo = m;
       CSS_OPAQUE_S(mo);
-#pragma unroll
-      for (int jj = 0; jj < MP; ++jj) A[jj] = (row && jj < mo) ? A[jj] : 0.0;
 #pragma unroll
       for (int s = 0; s < T80_TS; ++s) {
         const int j = 4 * s + tq;
@@ -440,46 +443,36 @@ __global__ void __launch_bounds__(64, 2)
     }
 
     CSS_PROF(0);
-    /* ---- fill_averages (k_css_mds) */
+    /* ---- fill_averages (k_css_mds).  The entries are exact integer counts, so "< 1e-5" is
+     * "== 0": sum = the plain row sum (zeros add nothing), the valid count = sum of
+     * min(v, 1), unval = m^2 - valid -- no per-entry branch or select (the branchy form
+     * compiled to ~25 instructions per entry) */
     {
-      /* the lane indices rebuilt for this phase (css_lane_now): kept live from the kernel's
-       * start they were spilled at the Householder steps' register peak and reloaded here */
       const int ln_ = css_lane_now();
-      const int i = ln_, tr = ln_ >> 2, tq = ln_ & 3;
-      const bool row = i < m, trow = T80_MAIN + tr < m;
-      int unval = 0;
-      double sum = 0;
-      int mo = m;
-      CSS_OPAQUE_S(mo);
+      const int tr = ln_ >> 2, tq = ln_ & 3;
+      double s4[4] = {0.0, 0.0, 0.0, 0.0}, n4[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
       for (int jj = 0; jj < MP; ++jj) {
-        if (row && jj < mo) {
-          if (A[jj] < 0.00001)
-            ++unval;
-          else
-            sum += A[jj];
-        }
+        s4[jj & 3] += A[jj];
+        n4[jj & 3] += fmin(A[jj], 1.0);
       }
 #pragma unroll
       for (int s = 0; s < T80_TS; ++s) {
-        const int j = 4 * s + tq;
-        const double t = s_tail[tr][j];
-        if (trow && j < mo) {
-          if (t < 0.00001)
-            ++unval;
-          else
-            sum += t;
-        }
+        const double t = s_tail[tr][4 * s + tq];
+        s4[s & 3] += t;
+        n4[s & 3] += fmin(t, 1.0);
       }
-      double unv = (double)unval;
-      wave_sum2(unv, sum); /* sums of integers: exact in any order */
-      unval = (int)unv;
+      double sum = (s4[0] + s4[1]) + (s4[2] + s4[3]), nz = (n4[0] + n4[1]) + (n4[2] + n4[3]);
+      wave_sum2(nz, sum); /* sums of integers: exact in any order */
       const int tot = m * m;
+      const int unval = tot - (int)nz;
       if (unval > tot / 2) continue; /* discarded window: outputs untouched */
       const double avg = sum / tot;
+      /* rows >= m stay zero; the columns >= m it fills are zeroed by the next pass */
+      const double avgr = ln_ < m ? avg : 0.0;
       CSS_OPAQUE_ROW(A);
 #pragma unroll
-      for (int jj = 0; jj < MP; ++jj) A[jj] = fma(avg, 1.0 - fmin(A[jj], 1.0), A[jj]);
+      for (int jj = 0; jj < MP; ++jj) A[jj] = fma(avgr, 1.0 - fmin(A[jj], 1.0), A[jj]);
 #pragma unroll
       for (int s = 0; s < T80_TS; ++s) {
         double *t = &s_tail[tr][4 * s + tq];
