@@ -1375,36 +1375,28 @@ __global__ void __launch_bounds__(64, CSS_P40_WAVES)
   /* ---- fill_averages per window (k_css_mds) */
   double avg;
   {
-    int un = 0;
-    double sm = 0;
-    int mo = mm;
-    CSS_OPAQUE_V(mo);
+    /* the entries are exact integer counts, zero outside the window's m x m (masked above):
+     * "< 1e-5" is "== 0", so the valid sum is the plain sum and the count of nonzero
+     * entries the sum of min(v, 1) -- no per-entry branch (k_css_mds_t80) */
+    double s4[2] = {0.0, 0.0}, n4[2] = {0.0, 0.0};
 #pragma unroll
     for (int jj = 0; jj < MP; ++jj) {
-      if (row && jj < mo) {
-        if (A[jj] < 0.00001)
-          ++un;
-        else
-          sm += A[jj];
-      }
+      s4[jj & 1] += A[jj];
+      n4[jj & 1] += fmin(A[jj], 1.0);
     }
 #pragma unroll
     for (int s = 0; s < H40_TS; ++s) {
-      const int j = 4 * s + tq;
-      const double t = s_tail[hi][tr][j];
-      if (trow && j < mo) {
-        if (t < 0.00001)
-          ++un;
-        else
-          sm += t;
-      }
+      const double t = s_tail[hi][tr][4 * s + tq];
+      s4[s & 1] += t;
+      n4[s & 1] += fmin(t, 1.0);
     }
-    double us = (double)un, ss = sm;
-    half_sum2(us, ss); /* sums of integers: exact in any order */
-    const double u2[2] = {readlane_f64(us, 0), readlane_f64(us, 32)};
+    double nz = n4[0] + n4[1], ss = s4[0] + s4[1];
+    half_sum2(nz, ss); /* sums of integers: exact in any order */
+    const double n2[2] = {readlane_f64(nz, 0), readlane_f64(nz, 32)};
 #pragma unroll
     for (int x = 0; x < 2; ++x) {
-      if (M[x] != 0 && (int)u2[x] > (M[x] * M[x]) / 2) M[x] = 0; /* discarded window: outputs untouched */
+      const int tot = M[x] * M[x];
+      if (M[x] != 0 && tot - (int)n2[x] > tot / 2) M[x] = 0; /* discarded window: outputs untouched */
     }
     avg = mm > 0 ? ss / (mm * mm) : 0.0;
   }
