@@ -56,7 +56,7 @@ FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 vector spec
 # tools/ubench_valu.hip: v_lshrrev_b32, v_add_f32, v_max_u16 ... 880-994 G/s at the held ~2.1 GHz).
 # Multiplies, FP64 and VOP3 three-source ops are 4-cycle: a kernel made of them tops out at 0.5.
 VALU_PEAK_GINSTS = 1024 * 2.4 / 2
-PROFILE_ROUND = "r05"
+PROFILE_ROUND = "r06"
 PROF = ROOT / "profiles"
 TRAFFIC_FILE = PROF / f"{PROFILE_ROUND}_fet_traffic.json"
 VALU_FILE = PROF / f"{PROFILE_ROUND}_fet_valu.json"

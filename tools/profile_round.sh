@@ -11,7 +11,7 @@
 #     kernels, and the C5 matrix-core busy cycles;
 #   phase cycles of the GD_CSS_PROFILE (varlib/cssprof) and GD_PERM_PROFILE (varlib/pprof)
 #     builds at the C3 / C4 / C5 shapes.  Build the two variants first:
-#       tools/build_variant.sh cssprof -DGD_CSS_PROFILE
+#       SRC="gd_css_t80 gd_css_h40" tools/build_variant.sh cssprof -DGD_CSS_PROFILE
 #       SRC=gd_css_perm tools/build_variant.sh pprof -DGD_PERM_PROFILE
 # Every GPU step has its own time limit; the steps are chained with &&.
 # usage: tools/profile_round.sh r05    (then: python tools/summarize_prof.py r05)
