@@ -130,15 +130,22 @@ struct PermShape {
   static constexpr bool MF = PERM_MFMA && MP <= 80;
   static constexpr int MT = (MP + 31) / 32, KT = (MP + 15) / 16;
   static constexpr int RS = KT * 32 + 16;
-  static constexpr int S16 = MT * 32 * RS; /* bytes of the fp16 matrix */
+  /* rows of the fp16 matrix: the last row tile's rows at and past MP read row MP, which stays
+   * zero (score_mfma clamps the fragment row), so the rows MP + 1 .. 32 MT - 1 take no LDS:
+   * at 80 individuals 81 rows instead of 96, and with the members' serial-stream start states
+   * computed per lane and no FP64-triangle alias the workgroup fits 6 per CU instead of 5 */
+  static constexpr int S16ROWS = MT * 32 > MP ? MP + 1 : MT * 32;
+  static constexpr int S16 = S16ROWS * RS; /* bytes of the fp16 matrix */
   /* region U: the FP64 triangle while a window is set up; then either the FP32 triangle,
    * the byte matrices and the member lists (FP32 score), or the fp16 matrix,
    * the byte matrices and the serial-stream start states (matrix-core score) */
   static constexpr int OFF_SIG = MF ? S16 : (TRI * 4 + 15) / 16 * 16;
   static constexpr int OFF_MEM = OFF_SIG + NWV * SIG;
-  static constexpr int MEMB = MF ? (NT + 1) * 8 : NWV * MEM;
-  static constexpr int UBYTES = OFF_MEM + MEMB > TRI * 8 ? OFF_MEM + MEMB : TRI * 8;
-  static_assert(MEMB >= (NT + 1) * 8, "the serial-stream start states alias the member lists");
+  /* matrix-core tiers: score_exact_wave's 256-byte scratch per wave; FP32 tiers: the member
+   * lists, which the serial-stream start states alias */
+  static constexpr int MEMB = MF ? NWV * 256 : NWV * MEM;
+  static constexpr int UBYTES = MF ? OFF_MEM + MEMB : (OFF_MEM + MEMB > TRI * 8 ? OFF_MEM + MEMB : TRI * 8);
+  static_assert(MF || MEMB >= (NT + 1) * 8, "the serial-stream start states alias the member lists");
 };
 
 /* packed lower triangle with one zero row appended: pair (x, y), x != y, at
@@ -524,8 +531,9 @@ __device__ __forceinline__ void score_mfma(const char *s16, const uint2 *lut, co
         v.z = h4.x;
         v.w = h4.y;
         const pm_f16x8 bf = __builtin_bit_cast(pm_f16x8, v);
+        const int arow = SH::S16ROWS < MT * 32 ? min(t * 32 + r, MP) : t * 32 + r; /* row MP is zero */
         const pm_f16x8 ah =
-            __builtin_bit_cast(pm_f16x8, *reinterpret_cast<const uint4 *>(s16 + (t * 32 + r) * RS + 2 * k0));
+            __builtin_bit_cast(pm_f16x8, *reinterpret_cast<const uint4 *>(s16 + arow * RS + 2 * k0));
         acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bf, acc, 0, 0, 0);
         if (kt & 1) asm volatile("" ::: "memory"); /* two k steps of fragment loads in flight */
       }
@@ -767,10 +775,10 @@ __device__ __forceinline__ bool fy_fast_unrolled(uint8_t *col, uint64_t x) {
 }
 
 /* the same with random_int_nrand48's redraw loop (css.c:675-690) */
-__device__ __forceinline__ void fy_exact(uint8_t *col, uint64_t x, int m, const uint32_t *mag) {
+__device__ __forceinline__ void fy_exact(uint8_t *col, uint64_t x, int m) {
   for (int s = 0; s < m - 1; ++s) {
     const int n = __builtin_amdgcn_readfirstlane(m - s);
-    const gd_randint rd = perm_rd((uint32_t)n, __builtin_amdgcn_readfirstlane(mag[n]));
+    const gd_randint rd = gd_randint_make((uint32_t)n);
     uint32_t r;
     do {
       x = gd_lcg_next(x);
@@ -783,6 +791,20 @@ __device__ __forceinline__ void fy_exact(uint8_t *col, uint64_t x, int m, const 
   }
 }
 
+
+/* the exact serial stream (random_int_nrand48's redraws, css.c:675-690) advanced over q whole
+ * permutations of m - 1 draws each: a permutation's start state, derived by its own lane (the
+ * rare rejection path) */
+__device__ __forceinline__ uint64_t serial_advance(uint64_t y, int q, int m, uint32_t vm0, uint32_t vm1) {
+  for (int p = 0; p < q; ++p)
+    for (int s = 0; s < m - 1; ++s) {
+      const int n = __builtin_amdgcn_readfirstlane(m - s);
+      const gd_randint rd = perm_rd((uint32_t)n, perm_mag(vm0, vm1, n));
+      do y = gd_lcg_next(y);
+      while (gd_lcg_value(y) > rd.limit);
+    }
+  return y;
+}
 
 /* sum over the wave, the same value in every lane (an xor butterfly: both lanes of a
  * pair add the same two operands) */
@@ -880,8 +902,11 @@ __global__ void __launch_bounds__(PermShape<MP>::NT) PERM_WPE
   using SH = PermShape<MP>;
   constexpr int TRI = SH::TRI, NWV = SH::NWV, NT = SH::NT, P = 64 * NWV, SIG = SH::SIG;
   __shared__ __attribute__((aligned(16))) char s_U[SH::UBYTES];
-  __shared__ double s_X[2 * MP]; /* the window's MDS coordinates (FP64 distances on demand) */
-  __shared__ double s_R[MP + 1];
+  /* the window's MDS coordinates (FP64 distances on demand): the FP32 tiers stage them in
+   * LDS; the matrix-core tiers read them in place (xbuf; the window setup and the rare
+   * near-tie recomputes only), which keeps their workgroup at 6 per CU */
+  __shared__ double s_Xl[SH::MF ? 1 : 2 * MP];
+  __shared__ double s_R[SH::MF ? 1 : MP + 1]; /* row sums: the FP32 score's tiers only */
   __shared__ uint64_t s_hit[NWV];
   __shared__ uint8_t s_car[MP > 64 ? 128 : 64];
   __shared__ uint8_t s_gend[NWV * PERM_CHAINS * MP]; /* each chain's last composition */
@@ -889,10 +914,9 @@ __global__ void __launch_bounds__(PermShape<MP>::NT) PERM_WPE
   __shared__ int64_t s_w;
   double *s_S = reinterpret_cast<double *>(s_U); /* FP64 triangle: window setup only */
   float *s_S32 = reinterpret_cast<float *>(s_U);  /* FP32 triangle: the permutation passes */
-  uint64_t *s_st = reinterpret_cast<uint64_t *>(s_U + SH::OFF_MEM); /* serial start states (draw phase only) */
+  uint64_t *s_st = reinterpret_cast<uint64_t *>(s_U + SH::OFF_MEM); /* serial start states (FP32 tiers, draw phase only) */
+  __shared__ uint64_t s_next; /* the serial stream after a pass (matrix-core tiers' rejection path) */
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  __shared__ uint32_t s_mag[MP + 1]; /* random_int_nrand48 magic numbers (perm_rd) */
-  for (int n = tid; n <= MP; n += NT) s_mag[n] = gd_randint_make(n < 1 ? 1u : (uint32_t)n).magic;
   __shared__ uint2 s_lut[16]; /* 4 indicator bits -> 4 bf16 (0 or 1.0): score_mfma's B fragments */
   if (tid < 16) /* fp16 1.0 = 0x3C00 */
     s_lut[tid] = make_uint2((tid & 1 ? 0x3C00u : 0u) | (tid & 2 ? 0x3C000000u : 0u),
@@ -900,7 +924,8 @@ __global__ void __launch_bounds__(PermShape<MP>::NT) PERM_WPE
   __syncthreads();
   /* the magic numbers in VGPR lanes for fy_fast (kept for the kernel's life; the opaque
    * use completes the loads here, so the draw loop carries no LDS wait for them) */
-  uint32_t vm0 = lane <= MP ? s_mag[lane] : 0u, vm1 = lane + 64 <= MP ? s_mag[lane + 64] : 0u;
+  uint32_t vm0 = lane <= MP ? gd_randint_make(lane < 1 ? 1u : (uint32_t)lane).magic : 0u;
+  uint32_t vm1 = lane + 64 <= MP ? gd_randint_make((uint32_t)(lane + 64)).magic : 0u;
   PERM_OPAQUE(vm0);
   PERM_OPAQUE(vm1);
   const char *s16 = s_U; /* score_mfma: the scaled fp16 matrix */
@@ -934,12 +959,11 @@ __global__ void __launch_bounds__(PermShape<MP>::NT) PERM_WPE
     double obs, inv_sc = 1.0; /* score_mfma: S was scaled by 1 / inv_sc */
     int ln = tid;
     PERM_OPAQUE(ln);
+    const double *s_X = SH::MF ? xbuf + w * 2 * MP : s_Xl;
     if constexpr (SH::MF) {
       /* matrix-core tiers: no FP64 triangle.  The scale from the coordinates' bounding
        * box (its diagonal D >= every distance, D < 2^ex), then the scaled fp16 matrix of
        * S, zero outside m x m and on the diagonal, and the observed score by the wave */
-      for (int e = ln; e < 2 * m; e += NT) s_X[e] = xbuf[w * 2 * MP + e];
-      __syncthreads();
       double x0 = __builtin_inf(), x1 = -__builtin_inf(), y0 = __builtin_inf(), y1 = -__builtin_inf();
       for (int i = lane; i < m; i += 64) {
         x0 = fmin(x0, s_X[2 * i]);
@@ -998,13 +1022,13 @@ __global__ void __launch_bounds__(PermShape<MP>::NT) PERM_WPE
       }
 #endif
       PERM_PROF(6); /* the fp16 matrix */
-      const gd_randint rb = perm_rd((uint32_t)(b > 1 ? b : 2), s_mag[b > 1 ? b : 2]);
+      const gd_randint rb = gd_randint_make((uint32_t)(b > 1 ? b : 2));
       obs = score_exact_wave<MP>([](int k) { return (uint32_t)k; }, s_X, a, b, inva, invb, lane, my_lst, rb);
       if (tid < m) s_car[tid] = (uint8_t)tid; /* tracks := identity */
       __syncthreads();
     } else {
       /* S (packed triangle, zero rows for individuals >= m) and its row sums */
-      for (int e = ln; e < 2 * m; e += NT) s_X[e] = xbuf[w * 2 * MP + e];
+      for (int e = ln; e < 2 * m; e += NT) s_Xl[e] = xbuf[w * 2 * MP + e];
       __syncthreads();
       /* entry e = T(h) + l of the triangle, e strided over the threads (independent
        * entries, no per-row loop): h from the float root of 8e + 1 (within one of the
@@ -1100,23 +1124,28 @@ __global__ void __launch_bounds__(PermShape<MP>::NT) PERM_WPE
 #endif
       if (__syncthreads_or(rej)) {
         /* exact serial stream: the start state of every permutation of the pass */
-        if (tid == 0) {
-          uint64_t y = base;
-          for (int q = 0; q < P; ++q) {
-            s_st[q] = y;
-            for (int s = 0; s < m1; ++s) {
-              const gd_randint rd = perm_rd((uint32_t)(m - s), s_mag[m - s]);
-              do y = gd_lcg_next(y);
-              while (gd_lcg_value(y) > rd.limit);
+        uint64_t mine;
+        if constexpr (SH::MF) {
+          /* every thread derives its own (a rare path: no LDS table of start states) */
+          mine = serial_advance(base, tid, m, vm0, vm1);
+          if (tid == NT - 1) s_next = serial_advance(mine, 1, m, vm0, vm1);
+        } else {
+          if (tid == 0) {
+            uint64_t y = base;
+            for (int q = 0; q < P; ++q) {
+              s_st[q] = y;
+              y = serial_advance(y, 1, m, vm0, vm1);
             }
+            s_st[P] = y;
           }
-          s_st[P] = y;
+          __syncthreads();
+          mine = s_st[tid];
         }
         __syncthreads();
         sig_identity<MP>(my_sig, m, lane);
         __syncthreads();
-        fy_exact(col, s_st[tid], m, s_mag);
-        base = s_st[P];
+        fy_exact(col, mine, m);
+        base = SH::MF ? s_next : s_st[P];
       } else {
         base = gd_affine_apply(JP, base);
       }
@@ -1238,7 +1267,7 @@ __global__ void __launch_bounds__(PermShape<MP>::NT) PERM_WPE
         /* the rare lanes inside the bound: exact score by the whole wave, one lane at a time */
         uint64_t amb = __ballot(hit < 0);
         if (amb) {
-          const gd_randint rb = perm_rd((uint32_t)(b > 1 ? b : 2), s_mag[b > 1 ? b : 2]);
+          const gd_randint rb = gd_randint_make((uint32_t)(b > 1 ? b : 2));
           while (amb) {
             const int L = __builtin_ctzll(amb);
             amb &= amb - 1;
