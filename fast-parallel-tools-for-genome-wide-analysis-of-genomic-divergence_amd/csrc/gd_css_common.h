@@ -439,17 +439,18 @@ __device__ __forceinline__ void bisect_top2(int m, double glo, double ghi, doubl
 }
 
 /* eigenvector e of T (0: largest, 1: second): partial-pivot LU of T - lam_e I (U in
- * s_lu[e], multipliers in s_x + e MP, pivots in s_piv[e]) and the start vector in
- * s_y[e]; one lane.  The serial chain carries its running values in registers; LDS
+ * s_lu[slot], multipliers in s_x + slot MP, pivots in s_piv[slot]) and the start vector in
+ * s_y[slot], slot = e unless given (one eigenvector at a time in one buffer); one lane.  The serial chain carries its running values in registers; LDS
  * holds only read-once factors. */
 template <int MP>
 __device__ __forceinline__ void invit_factor(int m, int e, const double *s_d, const double *s_e, const double *s_lam,
                                              double (*s_lu)[3][MP], double *s_x, uint8_t (*s_piv)[MP],
-                                             double (*s_y)[MP]) {
+                                             double (*s_y)[MP], int slot = -1) {
+  const int sl = slot < 0 ? e : slot;
   const double sig = s_lam[e];
-  double *U0 = s_lu[e][0], *U1 = s_lu[e][1], *U2 = s_lu[e][2];
-  double *ml = s_x + e * MP; /* elimination multipliers; s_x is free until X is formed */
-  uint8_t *pv = s_piv[e];
+  double *U0 = s_lu[sl][0], *U1 = s_lu[sl][1], *U2 = s_lu[sl][2];
+  double *ml = s_x + sl * MP; /* elimination multipliers; s_x is free until X is formed */
+  uint8_t *pv = s_piv[sl];
   double cc0 = s_d[0] - sig, cc1 = m > 1 ? s_e[0] : 0.0;
   /* four steps' operands are loaded together: the stores of a block cannot be crossed
    * by the compiler, so a load per step would wait out its LDS latency on the chain */
@@ -485,7 +486,7 @@ __device__ __forceinline__ void invit_factor(int m, int e, const double *s_d, co
   /* start vector: deterministic, not orthogonal to anything in practice */
   for (int k = 0; k < m; ++k) {
     const double f = (double)((k * 40503u + 977u * (unsigned)(e + 1)) & 1023u) / 1024.0;
-    s_y[e][k] = (e == 0 ? 1.0 : ((k & 1) ? -1.0 : 1.0)) * (0.5 + f);
+    s_y[sl][k] = (e == 0 ? 1.0 : ((k & 1) ? -1.0 : 1.0)) * (0.5 + f);
   }
 }
 
@@ -493,7 +494,7 @@ __device__ __forceinline__ void invit_factor(int m, int e, const double *s_d, co
  * place in s_y[e]; one lane */
 template <int MP>
 __device__ __forceinline__ void invit_solve(int m, int e, double (*s_lu)[3][MP], const double *s_x,
-                                            uint8_t (*s_piv)[MP], double (*s_y)[MP]) {
+                                            uint8_t (*s_piv)[MP], double (*s_y)[MP]) { /* e: the slot */
   double *y = s_y[e];
   const double *R0 = s_lu[e][0], *U1 = s_lu[e][1], *U2 = s_lu[e][2], *ml = s_x + e * MP;
   const uint8_t *pv = s_piv[e];

@@ -1180,18 +1180,27 @@ __global__ void __launch_bounds__(64, CSS_P40_WAVES)
                   double *xbuf, uint8_t *status, unsigned *flags) {
   constexpr int MP = P40;
   __shared__ __attribute__((aligned(16))) double s_tail[2][8][H40_TSTRIDE];
+  /* the phase buffers share one region (12 workgroups per CU: <= 13.6 KB in all): the
+   * distance build's masks / values and the Householder steps' row, v, w never live at once;
+   * the pivoted-LU fallback holds one eigenvector's factors at a time */
   __shared__ __attribute__((aligned(16))) union {
     struct {
       double e2[2][MP + 4]; /* bisection only (after the Householder steps) */
-      double row[2][MP + 2];
-      double v[2][MP], w[2][MP];
-      uint64_t mask[2][2 * MP];
-      double vals[2][MP];
+      union {
+        struct {
+          uint64_t mask[2][2 * MP];
+          double vals[2][MP];
+        };
+        struct {
+          double row[2][MP + 2];
+          double v[2][MP], w[2][MP];
+        };
+      };
     } a;
     struct {
-      double lu[2][2][3][MP];
-      double y[2][2][MP];
-      uint8_t piv[2][2][MP];
+      double lu[2][1][3][MP];
+      double y[2][2][MP]; /* [window][slot 0: the solve, slot 1: the first eigenvector] */
+      uint8_t piv[2][1][MP];
     } b;
     struct {
       double e2[2][MP + 4]; /* = a.e2: the twisted factorisations read it */
@@ -1549,54 +1558,51 @@ __global__ void __launch_bounds__(64, CSS_P40_WAVES)
   }
 #endif
   if (!twist_ok) {
-    if (lane < 4 && M[lane >> 1] > 0) {
-      const int x = lane >> 1, e = lane & 1;
-      invit_factor<MP>(M[x], e, s_d[x], s_e[x], s_lam[x], s_u.b.lu[x], s_x[x], s_u.b.piv[x], s_u.b.y[x]);
-    }
-    __syncthreads();
+    /* one eigenvector at a time in slot 0 (lane x of window x); the first one's unit vector
+     * waits in y[x][1] */
+#pragma unroll 1
+    for (int e = 0; e < 2; ++e) {
+      __syncthreads();
+      if (lane < 2 && M[lane] > 0)
+        invit_factor<MP>(M[lane], e, s_d[lane], s_e[lane], s_lam[lane], s_u.b.lu[lane], s_x[lane], s_u.b.piv[lane],
+                         s_u.b.y[lane], 0);
+      __syncthreads();
 #pragma unroll
-    for (int x = 0; x < 2; ++x) {
-      const double tiny = DBL_EPSILON * fmax(fmax(fabs(glo[x]), fabs(ghi[x])), DBL_MIN);
-      for (int k = lane; k < M[x]; k += 64) {
-#pragma unroll
-        for (int e = 0; e < 2; ++e) {
-          const double u0 = s_u.b.lu[x][e][0][k];
-          s_u.b.lu[x][e][0][k] = fast_rcp(u0 == 0.0 ? tiny : u0);
+      for (int x = 0; x < 2; ++x) {
+        const double tiny = DBL_EPSILON * fmax(fmax(fabs(glo[x]), fabs(ghi[x])), DBL_MIN);
+        for (int k = lane; k < M[x]; k += 64) {
+          const double u0 = s_u.b.lu[x][0][0][k];
+          s_u.b.lu[x][0][0][k] = fast_rcp(u0 == 0.0 ? tiny : u0);
         }
       }
-    }
+      double ye = 0.0, yet = 0.0;
 #ifdef GD_CSS_SKIP_INVIT
-    for (int itn = 0; itn < 0; ++itn) {
+      for (int itn = 0; itn < 0; ++itn) {
 #else
-    for (int itn = 0; itn < 2; ++itn) {
+      for (int itn = 0; itn < 2; ++itn) {
 #endif
-      __syncthreads();
-      if (lane < 4 && M[lane >> 1] > 0) {
-        const int x = lane >> 1;
-        invit_solve<MP>(M[x], lane & 1, s_u.b.lu[x], s_x[x], s_u.b.piv[x], s_u.b.y[x]);
+        __syncthreads();
+        if (lane < 2 && M[lane] > 0) invit_solve<MP>(M[lane], 0, s_u.b.lu[lane], s_x[lane], s_u.b.piv[lane], s_u.b.y[lane]);
+        __syncthreads();
+        ye = rowk ? s_u.b.y[hi][0][r] : 0.0;
+        yet = trowk ? s_u.b.y[hi][0][R] : 0.0;
+        double n1 = ye * ye + (tq == 0 ? yet * yet : 0.0), dm = 0.0;
+        half_sum2(n1, dm);
+        const double r1 = 1.0 / sqrt(n1);
+        ye *= r1;
+        yet *= r1;
+        __syncthreads();
+        if (itn == 0) {
+          if (rowk) s_u.b.y[hi][0][r] = ye;
+          if (tq == 0 && trowk) s_u.b.y[hi][0][R] = yet;
+        }
       }
-      __syncthreads();
-      y1 = rowk ? s_u.b.y[hi][0][r] : 0.0;
-      y2 = rowk ? s_u.b.y[hi][1][r] : 0.0;
-      y1t = trowk ? s_u.b.y[hi][0][R] : 0.0;
-      y2t = trowk ? s_u.b.y[hi][1][R] : 0.0;
-      double n1 = y1 * y1 + (tq == 0 ? y1t * y1t : 0.0), n2 = y2 * y2 + (tq == 0 ? y2t * y2t : 0.0);
-      half_sum2(n1, n2);
-      const double r1 = 1.0 / sqrt(n1), r2 = 1.0 / sqrt(n2);
-      y1 *= r1;
-      y2 *= r2;
-      y1t *= r1;
-      y2t *= r2;
-      __syncthreads();
-      if (itn == 0) {
-        if (rowk) {
-          s_u.b.y[hi][0][r] = y1;
-          s_u.b.y[hi][1][r] = y2;
-        }
-        if (tq == 0 && trowk) {
-          s_u.b.y[hi][0][R] = y1t;
-          s_u.b.y[hi][1][R] = y2t;
-        }
+      if (e == 0) {
+        y1 = ye;
+        y1t = yet;
+      } else {
+        y2 = ye;
+        y2t = yet;
       }
     }
   }
