@@ -203,7 +203,7 @@ __device__ __forceinline__ void t80_fstep(double (&A)[T80], int m, T80Carry &c, 
   }
   double tau = 0.0, beta = alpha, scale = 0.0;
   if (sigma != 0.0) {
-    beta = -copysign(sqrt(alpha * alpha + sigma), alpha);
+    beta = -copysign(sqrt_pos(alpha * alpha + sigma), alpha);
     const double rr = fast_rcp(beta * (alpha - beta));
     tau = -(alpha - beta) * (alpha - beta) * rr;
     scale = beta * rr;
