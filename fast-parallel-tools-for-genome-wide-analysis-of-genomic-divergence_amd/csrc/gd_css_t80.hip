@@ -69,14 +69,15 @@ __device__ __forceinline__ void t80_fused_pass(double (&A)[T80], double vi, doub
 #pragma unroll
     for (int u = 0; u < FB; ++u) {
       const int j = FB * jb + u;
-      if (j > K) A[j] = fma(-vi, cvw[u].y, fma(-wi, cvw[u].x, A[j]));
+      /* from K = 63 on every main row is finished (v_i = w_i = 0): no update */
+      if (j > K && K + 1 < T80_MAIN) A[j] = fma(-vi, cvw[u].y, fma(-wi, cvw[u].x, A[j]));
     }
 #pragma unroll
     for (int u = 0; u < FB; ++u) CSS_PIN(A[FB * jb + u]);
 #pragma unroll
     for (int u = 0; u < FB; ++u) {
       const int j = FB * jb + u;
-      if (j > K + 1) p[u & 3] = fma(A[j], cr[u], p[u & 3]);
+      if (j > K + 1 && K + 1 < T80_MAIN) p[u & 3] = fma(A[j], cr[u], p[u & 3]);
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) CSS_PIN(p[u]);
@@ -184,12 +185,13 @@ template <int K>
 __device__ __forceinline__ void t80_fstep(double (&A)[T80], int m, T80Carry &c, double2 *s_vw, double *s_r,
                                           double *s_d, double *s_e, double *s_tau, double (*s_tail)[T80_TSTRIDE]) {
   const int i = css_lane_now(), tr = i >> 2, tq = i & 3, R = T80_MAIN + tr;
-  const bool row = i < m, trow = R < m;
-  const double xi = (i > K + 1 && row) ? c.r : 0.0;
-  const double xr = (R > K + 1 && trow) ? c.rt : 0.0;
+  /* rows >= m are zero and stay zero (v_i = w_i = 0 there), as do their r and p entries:
+   * only the rows the earlier steps finished (<= K) need masking */
+  const double xi = (i > K + 1) ? c.r : 0.0;
+  const double xr = (R > K + 1) ? c.rt : 0.0;
   /* |x|^2 and r^T A r in one reduction; a tail row counts once */
   double sigma = xi * xi + (tq == 0 ? xr * xr : 0.0);
-  double q = ((i > K && row) ? c.r * c.p : 0.0) + ((tq == 0 && R > K && trow) ? c.rt * c.pt : 0.0);
+  double q = ((i > K) ? c.r * c.p : 0.0) + ((tq == 0 && R > K) ? c.rt * c.pt : 0.0);
   wave_sum2(sigma, q);
   double alpha, pr1, a11;
   if constexpr (K + 1 < T80_MAIN) {
@@ -211,11 +213,11 @@ __device__ __forceinline__ void t80_fstep(double (&A)[T80], int m, T80Carry &c, 
   const double Kc = -0.5 * tau * (tau * scale * scale) * fma(beta, fma(beta, a11, -2.0 * pr1), q);
   const double ak1 = A[K + 1];
   const double vi = (i == K + 1) ? 1.0 : xi * scale;
-  const double pi = (i > K && row) ? (tau * scale) * fma(-beta, ak1, c.p) : 0.0;
+  const double pi = (i > K) ? (tau * scale) * fma(-beta, ak1, c.p) : 0.0;
   const double wi = fma(Kc, vi, pi);
   const double akt = s_tail[tr][K + 1];
   const double vt = (R == K + 1) ? 1.0 : xr * scale;
-  const double ptl = (R > K && trow) ? (tau * scale) * fma(-beta, akt, c.pt) : 0.0;
+  const double ptl = (R > K) ? (tau * scale) * fma(-beta, akt, c.pt) : 0.0;
   const double wt = fma(Kc, vt, ptl);
   double wk1;
   if constexpr (K + 1 < T80_MAIN)
