@@ -249,7 +249,7 @@ __global__ void __launch_bounds__(MP / R)
       const double pr1 = s_red[2 * NW], a11 = s_red[2 * NW + 1];
       double tau = 0.0, beta = alpha, scale = 0.0;
       if (sigma != 0.0) {
-        beta = -copysign(sqrt(alpha * alpha + sigma), alpha);
+        beta = -copysign(sqrt_pos(alpha * alpha + sigma), alpha);
         const double r = fast_rcp(beta * (alpha - beta));
         tau = -(alpha - beta) * (alpha - beta) * r;
         scale = beta * r;

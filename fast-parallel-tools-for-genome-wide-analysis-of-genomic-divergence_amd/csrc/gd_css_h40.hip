@@ -24,7 +24,7 @@ __device__ __forceinline__ void hh_scalars(double alpha, double sigma, double q,
                                            double *beta, double *scale, double *Kc) {
   double t = 0.0, be = alpha, sc = 0.0;
   if (sigma != 0.0) {
-    be = -copysign(sqrt(alpha * alpha + sigma), alpha);
+    be = -copysign(sqrt_pos(alpha * alpha + sigma), alpha);
     const double r = fast_rcp(be * (alpha - be));
     t = -(alpha - be) * (alpha - be) * r;
     sc = be * r;

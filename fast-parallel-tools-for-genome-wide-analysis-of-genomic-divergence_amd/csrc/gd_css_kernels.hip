@@ -142,7 +142,7 @@ __device__ __forceinline__ void hh_step_static(double (&A)[MP], int m, double *s
   const double pr1 = readlane_f64(praw, K + 1), a11 = readlane_f64(ak1, K + 1);
   double tau = 0.0, beta = alpha, scale = 0.0;
   if (sigma != 0.0) {
-    beta = -copysign(sqrt(alpha * alpha + sigma), alpha);
+    beta = -copysign(sqrt_pos(alpha * alpha + sigma), alpha);
     const double r = fast_rcp(beta * (alpha - beta)); /* 1/beta and 1/(alpha - beta) from one reciprocal */
     tau = -(alpha - beta) * (alpha - beta) * r;
     scale = beta * r;
@@ -282,7 +282,7 @@ __device__ __forceinline__ void hh_step_static_g(double (&A)[MP / G], int m, int
     const double pr1 = red[2 * NW], a11 = red[2 * NW + 1];
     double tau = 0.0, beta = alpha, scale = 0.0;
     if (sigma != 0.0) {
-      beta = -copysign(sqrt(alpha * alpha + sigma), alpha);
+      beta = -copysign(sqrt_pos(alpha * alpha + sigma), alpha);
       const double r = fast_rcp(beta * (alpha - beta));
       tau = -(alpha - beta) * (alpha - beta) * r;
       scale = beta * r;
@@ -606,7 +606,7 @@ __global__ void __launch_bounds__((CssShape<MP, G>::NT), CSS_MDS_WAVES(MP, G))
       }
       double tau = 0.0, beta = alpha, scale = 0.0;
       if (sigma != 0.0) {
-        beta = -copysign(sqrt(alpha * alpha + sigma), alpha);
+        beta = -copysign(sqrt_pos(alpha * alpha + sigma), alpha);
         const double r = fast_rcp(beta * (alpha - beta));
         tau = -(alpha - beta) * (alpha - beta) * r;
         scale = beta * r;

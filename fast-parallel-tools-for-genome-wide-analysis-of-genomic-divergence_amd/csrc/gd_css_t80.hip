@@ -691,13 +691,17 @@ __global__ void __launch_bounds__(64, 2)
     CSS_PROF(4);
     /* ---- back-transformation y <- H_0 H_1 ... H_{m-3} y; v_k sits in column k */
 #ifndef GD_CSS_SKIP_BACK
+    /* v_k is zero in rows >= m (k <= m - 3: the steps that left it there saw zero rows), so
+     * only the tail's quad replication needs a mask: one factor, no per-step selects */
+    const double tq0 = tq == 0 ? 1.0 : 0.0;
 #pragma unroll
     for (int k = MP - 3; k >= 0; --k) {
       if (k <= m - 3) {
-        const double vk = row ? A[k] : 0.0;
-        const double vkt = trow ? s_tail[tr][k] : 0.0;
+        const double vk = A[k];
+        const double vkt = s_tail[tr][k];
         const double t = s_tau[k];
-        double d1 = vk * y1 + (tq == 0 ? vkt * y1t : 0.0), d2 = vk * y2 + (tq == 0 ? vkt * y2t : 0.0);
+        const double vq = vkt * tq0;
+        double d1 = fma(vq, y1t, vk * y1), d2 = fma(vq, y2t, vk * y2);
         wave_sum2(d1, d2);
         y1 = fma(-(t * d1), vk, y1);
         y2 = fma(-(t * d2), vk, y2);
