@@ -248,6 +248,9 @@ __device__ __forceinline__ double swap32_sum(double v) {
   return __builtin_bit_cast(double, ((uint64_t)h[0] << 32) | l[0]) +
          __builtin_bit_cast(double, ((uint64_t)h[1] << 32) | l[1]);
 }
+#ifndef CSS_SUM2_LDS
+#define CSS_SUM2_LDS 0 /* measured slower (C4 9.92 -> 9.62 M windows/s): LDS latency on the chain */
+#endif
 /* Two wave sums in ONE reduction chain.  The first step splits the work by lane bit 3:
  * lanes 0-7 of every row keep a, lanes 8-15 keep b, and each lane receives the value of its
  * class from its row_mirror partner (lane 15 - i, the other class).  The remaining steps
@@ -263,7 +266,23 @@ __device__ __forceinline__ void wave_sum2(double &a, double &b) {
   v += dpp64<0xB1, 0xF>(v, 0.0);     /* quad_perm [1,0,3,2] */
   v += dpp64<0x4E, 0xF>(v, 0.0);     /* quad_perm [2,3,0,1] */
   v += dpp64<0x141, 0xF>(v, 0.0);    /* row_half_mirror */
+#if CSS_SUM2_LDS
+  /* the cross-row steps through the LDS crossbar (ds_swizzle lane ^ 16, ds_bpermute lane ^ 32):
+   * one VALU add each instead of two copies, two swaps and the add */
+  {
+    uint64_t u = __builtin_bit_cast(uint64_t, v);
+    const uint32_t l16 = (uint32_t)__builtin_amdgcn_ds_swizzle((int)(uint32_t)u, 0x401F);
+    const uint32_t h16 = (uint32_t)__builtin_amdgcn_ds_swizzle((int)(uint32_t)(u >> 32), 0x401F);
+    v += __builtin_bit_cast(double, ((uint64_t)h16 << 32) | l16);
+    u = __builtin_bit_cast(uint64_t, v);
+    const int src = (int)((__lane_id() ^ 32u) << 2);
+    const uint32_t l32 = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)u);
+    const uint32_t h32 = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)(u >> 32));
+    v += __builtin_bit_cast(double, ((uint64_t)h32 << 32) | l32);
+  }
+#else
   v = swap32_sum(swap16_sum(v));
+#endif
   a = readlane_f64(v, 0);
   b = readlane_f64(v, 8);
 }
