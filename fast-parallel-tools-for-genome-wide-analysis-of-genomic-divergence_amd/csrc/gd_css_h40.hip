@@ -1090,13 +1090,13 @@ __device__ __forceinline__ void h40_fstep(double (&A)[P40], const int (&M)[2], H
   const int lane = css_lane_now();
   const bool h = lane >= 32;
   const int hi = h ? 1 : 0, r = lane & 31, tr = r >> 2, tq = lane & 3, R = H40_MAIN + tr;
-  const int mine = h ? M[1] : M[0];
-  const bool row = r < mine, trow = R < mine;
-  const double xi = (r > K + 1 && row) ? c.r : 0.0;
-  const double xr = (R > K + 1 && trow) ? c.rt : 0.0;
+  /* rows >= m of a window are zero and stay zero (their v, w, r and p are zero, k_css_mds_t80):
+   * only the rows the earlier steps finished (<= K) need masking */
+  const double xi = (r > K + 1) ? c.r : 0.0;
+  const double xr = (R > K + 1) ? c.rt : 0.0;
   /* |x|^2 and r^T A r of each window in one half-wave sum; a tail row counts once */
   double sigma = xi * xi + (tq == 0 ? xr * xr : 0.0);
-  double q = ((r > K && row) ? c.r * c.p : 0.0) + ((tq == 0 && R > K && trow) ? c.rt * c.pt : 0.0);
+  double q = ((r > K) ? c.r * c.p : 0.0) + ((tq == 0 && R > K) ? c.rt * c.pt : 0.0);
   half_sum2(sigma, q);
   double alpha, pr1, a11;
   if constexpr (K + 1 < H40_MAIN) {
@@ -1112,11 +1112,11 @@ __device__ __forceinline__ void h40_fstep(double (&A)[P40], const int (&M)[2], H
   hh_scalars(alpha, sigma, q, pr1, a11, &tau, &beta, &scale, &Kc);
   const double ak1 = A[K + 1];
   const double vi = (r == K + 1) ? 1.0 : xi * scale;
-  const double pi = (r > K && row) ? (tau * scale) * fma(-beta, ak1, c.p) : 0.0;
+  const double pi = (r > K) ? (tau * scale) * fma(-beta, ak1, c.p) : 0.0;
   const double wi = fma(Kc, vi, pi);
   const double akt = s_tail[hi][tr][K + 1];
   const double vt = (R == K + 1) ? 1.0 : xr * scale;
-  const double ptl = (R > K && trow) ? (tau * scale) * fma(-beta, akt, c.pt) : 0.0;
+  const double ptl = (R > K) ? (tau * scale) * fma(-beta, akt, c.pt) : 0.0;
   const double wt = fma(Kc, vt, ptl);
   double wk1;
   if constexpr (K + 1 < H40_MAIN)
@@ -1658,16 +1658,20 @@ __global__ void __launch_bounds__(64, CSS_P40_WAVES)
   CSS_PROF(4);
   /* ---- back-transformation y <- H_0 H_1 ... H_{m-3} y per window */
 #ifndef GD_CSS_SKIP_BACK
+  const double tq0 = tq == 0 ? 1.0 : 0.0;
 #pragma unroll
   for (int k = MP - 3; k >= 0; --k) {
     const bool liveA = k <= M[0] - 3, liveB = k <= M[1] - 3;
     if (liveA || liveB) {
+      /* a window past its last reflector only needs tau = 0 (its y stays); rows past m hold
+       * zero v, and the tail's quad replication is one 0/1 factor (k_css_mds_t80) */
       const bool mine = h ? liveB : liveA;
-      const double vk = (rowk && mine) ? A[k] : 0.0;
-      const double vkt = (trowk && mine) ? s_tail[hi][tr][k] : 0.0;
+      const double vk = A[k];
+      const double vkt = s_tail[hi][tr][k];
       const double t = mine ? s_tau[hi][k] : 0.0;
-      double d1 = vk * y1 + (tq == 0 ? vkt * y1t : 0.0);
-      double d2 = vk * y2 + (tq == 0 ? vkt * y2t : 0.0);
+      const double vq = vkt * tq0;
+      double d1 = fma(vq, y1t, vk * y1);
+      double d2 = fma(vq, y2t, vk * y2);
       half_sum2(d1, d2);
       y1 = fma(-(t * d1), vk, y1);
       y2 = fma(-(t * d2), vk, y2);
