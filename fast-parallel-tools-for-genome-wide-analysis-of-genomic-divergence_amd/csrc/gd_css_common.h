@@ -637,7 +637,29 @@ __device__ __forceinline__ void half_reduce2(double &a, double &b) {
   b = Op::op(__builtin_bit_cast(double, ((uint64_t)bh[0] << 32) | bl[0]),
              __builtin_bit_cast(double, ((uint64_t)bh[1] << 32) | bl[1]));
 }
-__device__ __forceinline__ void half_sum2(double &a, double &b) { half_reduce2<OpSum>(a, b); }
+#ifndef CSS_HALF_SPLIT
+#define CSS_HALF_SPLIT 1
+#endif
+/* two sums over each 32-lane half, every lane of a half ending with both (the same bits):
+ * CSS_HALF_SPLIT runs them as ONE chain split by lane bit 3 (wave_sum2's scheme), then the
+ * row_mirror partner hands each lane the other class's sum -- 27 VALU instead of 34 */
+__device__ __forceinline__ void half_sum2(double &a, double &b) {
+#if CSS_HALF_SPLIT
+  constexpr uint64_t B3 = 0xFF00FF00FF00FF00ull;
+  double v = sel_mask(a, b, B3);
+  const double send = sel_mask(b, a, B3);
+  v += dpp64<0x140, 0xF>(send, 0.0); /* row_mirror */
+  v += dpp64<0xB1, 0xF>(v, 0.0);     /* quad_perm [1,0,3,2] */
+  v += dpp64<0x4E, 0xF>(v, 0.0);     /* quad_perm [2,3,0,1] */
+  v += dpp64<0x141, 0xF>(v, 0.0);    /* row_half_mirror */
+  v = swap16_sum(v);
+  const double o = dpp64<0x140, 0xF>(v, 0.0);
+  a = sel_mask(v, o, B3);
+  b = sel_mask(o, v, B3);
+#else
+  half_reduce2<OpSum>(a, b);
+#endif
+}
 
 /* Eigenvectors of T for the shifts sig0 / sig1 (the two bisection results) by twisted
  * factorisations T - sig I = N_r Delta_r N_r^T (Parlett & Dhillon's solution of

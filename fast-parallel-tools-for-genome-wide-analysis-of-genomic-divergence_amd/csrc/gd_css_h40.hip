@@ -17,6 +17,9 @@ constexpr int P40 = 40, P40_BMAIN = 24, P40_TS = 10; /* order, B rows in VGPRs, 
 /* tail row stride in doubles: 2 * 44 = 24 (mod 64) dwords, so the 8 tail rows of a 32-lane
  * group start 8 banks apart (k_css_mds_t80) */
 constexpr int P40_TSTRIDE = 44;
+#ifndef H40_BPERM
+#define H40_BPERM 1
+#endif
 
 /* the Householder scalars of one window from its reduced |x|^2 (sigma), r^T A r (q),
  * (A r)_{K+1} (pr1) and A_{K+1,K+1} (a11) -- hh_step_static's recurrences */
@@ -818,6 +821,16 @@ __device__ __forceinline__ double half_lane(double v, int L, bool h) {
   const double v0 = readlane_f64(v, L), v1 = readlane_f64(v, 32 + L);
   return h ? v1 : v0;
 }
+/* the same through the LDS crossbar: two ds_bpermute from lane (lane & 32) + L, no VALU but the
+ * address (k_css_mds_h40 is VALU-bound: four readlanes, two moves and two selects per value
+ * cost more than the LDS latency, which the half-wave sums beside these reads cover) */
+__device__ __forceinline__ double half_bperm(double v, int L, int lane) {
+  const int addr = ((lane & 32) + L) << 2;
+  const uint64_t u = __builtin_bit_cast(uint64_t, v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute(addr, (int)(uint32_t)u);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute(addr, (int)(uint32_t)(u >> 32));
+  return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
 
 template <int K>
 __device__ __forceinline__ void h40_step(double (&A)[P40], const int (&M)[2], double (*s_row)[P40 + 2],
@@ -1099,6 +1112,17 @@ __device__ __forceinline__ void h40_fstep(double (&A)[P40], const int (&M)[2], H
   double q = ((r > K) ? c.r * c.p : 0.0) + ((tq == 0 && R > K) ? c.rt * c.pt : 0.0);
   half_sum2(sigma, q);
   double alpha, pr1, a11;
+#if H40_BPERM
+  if constexpr (K + 1 < H40_MAIN) {
+    alpha = half_bperm(c.r, K + 1, lane);
+    pr1 = half_bperm(c.p, K + 1, lane);
+    a11 = half_bperm(A[K + 1], K + 1, lane);
+  } else {
+    alpha = half_bperm(c.rt, 4 * (K + 1 - H40_MAIN), lane);
+    pr1 = half_bperm(c.pt, 4 * (K + 1 - H40_MAIN), lane);
+    a11 = s_tail[hi][K + 1 - H40_MAIN][K + 1];
+  }
+#else
   if constexpr (K + 1 < H40_MAIN) {
     alpha = half_lane(c.r, K + 1, h);
     pr1 = half_lane(c.p, K + 1, h);
@@ -1108,6 +1132,7 @@ __device__ __forceinline__ void h40_fstep(double (&A)[P40], const int (&M)[2], H
     pr1 = half_lane(c.pt, 4 * (K + 1 - H40_MAIN), h);
     a11 = s_tail[hi][K + 1 - H40_MAIN][K + 1];
   }
+#endif
   double tau, beta, scale, Kc;
   hh_scalars(alpha, sigma, q, pr1, a11, &tau, &beta, &scale, &Kc);
   const double ak1 = A[K + 1];
@@ -1118,11 +1143,16 @@ __device__ __forceinline__ void h40_fstep(double (&A)[P40], const int (&M)[2], H
   const double vt = (R == K + 1) ? 1.0 : xr * scale;
   const double ptl = (R > K) ? (tau * scale) * fma(-beta, akt, c.pt) : 0.0;
   const double wt = fma(Kc, vt, ptl);
+#if H40_BPERM
+  /* w at row K + 1 as that lane forms it (v = 1 there, p from the scalars): the same bits */
+  const double wk1 = fma(Kc, 1.0, (tau * scale) * fma(-beta, a11, pr1));
+#else
   double wk1;
   if constexpr (K + 1 < H40_MAIN)
     wk1 = half_lane(wi, K + 1, h);
   else
     wk1 = half_lane(wt, 4 * (K + 1 - H40_MAIN), h);
+#endif
   /* column K + 1 after this step (the update's formula at v_{K+1} = 1) */
   const double rn = fma(-vi, wk1, fma(-wi, 1.0, ak1));
   const double rnt = fma(-vt, wk1, fma(-wt, 1.0, akt));
