@@ -95,7 +95,10 @@ __device__ __forceinline__ void t80_fused_pass(double (&A)[T80], double vi, doub
   A[K] = vi; /* stash v_K in the dead column K */
   double *tw = s_tail[tr];
   double t0 = 0.0, t1 = 0.0;
-  constexpr int TG = 2, S0 = (K + 1) / 4 / TG * TG; /* tail groups of TG column quads */
+#ifndef T80_TG
+#define T80_TG 2
+#endif
+  constexpr int TG = T80_TG, S0 = (K + 1) / 4 / TG * TG; /* tail groups of TG column quads */
   double ct[TG], ctr[TG];
   double2 ctv[TG];
   /* the odd member of each column pair is addressed through an opaque zero, so the two 8-byte
