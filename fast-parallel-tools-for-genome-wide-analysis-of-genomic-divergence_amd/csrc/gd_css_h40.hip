@@ -996,7 +996,10 @@ __device__ __forceinline__ void h40_fused_pass(double (&A)[P40], double vi, doub
   constexpr int MP = P40;
   const int lane = css_lane_now(), tr = (lane & 31) >> 2, tq = lane & 3;
   double p[4] = {0.0, 0.0, 0.0, 0.0};
-  constexpr int FB = 4; /* columns per pinned group */
+#ifndef H40_FB
+#define H40_FB 4
+#endif
+  constexpr int FB = H40_FB; /* columns per pinned group */
   constexpr int NB = MP / FB, JB0 = (K + 1) / FB;
   double2 cvw[FB];
   double cr[FB];
